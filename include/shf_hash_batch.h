@@ -1,0 +1,142 @@
+/*
+ * shf_hash_batch.h -- C ABI of the MI355X batch key-hashing stage for
+ * SharedHashFile.
+ *
+ * What it replaces. SharedHashFile hashes one key per call:
+ *
+ *     extern void shf_make_hash(const char *key, uint32_t key_len);
+ *                                         -- /root/reference/src/shf.h:381
+ *     -> MurmurHash3_x64_128(key, key_len, 12345, &shf_hash.u64[0])
+ *                                         -- /root/reference/src/shf.c:456,
+ *                                            /root/reference/src/murmurhash3.c:75
+ *     result in the thread-local SHF_HASH shf_hash (u64[0] = h1, u64[1] = h2)
+ *                                         -- /root/reference/src/shf.private.h:180-189
+ *
+ * The functions below compute the same 16 bytes for a whole batch of keys on
+ * the GPU, bit-exact, and write them as an array of SHF_HASH-layout records
+ * (struct shf_hash128). The results re-enter the unchanged put/get/del flow
+ * through the reference's caller-supplied-hash seam: set shf_hash,
+ * shf_hash_key and shf_hash_key_len per key and call shf_put_key_val() /
+ * shf_get_key_val_copy() / shf_del_key_val() (as
+ * /root/reference/src/test.9.shf.c:176-182 does). INTEGRATION.md shows the
+ * helper a maintainer adds for that.
+ *
+ * Conventions.
+ *   - Plain pointers and sizes only; no HIP or C++ types cross this ABI
+ *     (streams are passed as `void *` holding a hipStream_t).
+ *   - Every function returns SHF_HB_OK (0) or a negative SHF_HB_ERR_* code;
+ *     nothing aborts. shf_hash_batch_strerror() names a code.
+ *   - There is no CPU fallback: without a usable gfx950 device every hashing
+ *     call returns SHF_HB_ERR_NODEV (or SHF_HB_ERR_ARCH).
+ *   - Thread-safe: each calling thread gets its own HIP streams and staging
+ *     buffers per device. Device selection follows the calling thread's
+ *     current HIP device (hipSetDevice), as HIP itself does.
+ *   - Key lengths follow the reference's `const int len` parameter
+ *     (murmurhash3.c:75): key_len and every variable key length must be
+ *     < 2^31, else SHF_HB_ERR_ARG.
+ */
+#ifndef SHF_HASH_BATCH_H
+#define SHF_HASH_BATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define SHF_HB_API __attribute__((visibility("default")))
+#else
+#define SHF_HB_API
+#endif
+
+/* Seed shf_make_hash() uses (/root/reference/src/shf.c:456). */
+#define SHF_HASH_BATCH_SEED 12345u
+
+/* Status codes. */
+#define SHF_HB_OK 0
+#define SHF_HB_ERR_ARG (-1)    /* bad argument: NULL buffer with n > 0, key length >= 2^31, bad mem kind */
+#define SHF_HB_ERR_NODEV (-2)  /* no HIP device / runtime available */
+#define SHF_HB_ERR_HIP (-3)    /* a HIP call failed; shf_hash_batch_last_hip_error() has the hipError_t */
+#define SHF_HB_ERR_NOMEM (-4)  /* device or pinned-host allocation failed */
+#define SHF_HB_ERR_ARCH (-5)   /* current device is not gfx950 (MI355X) */
+
+/* Where the caller's buffers live. */
+#define SHF_HASH_MEM_DEVICE 0 /* keys, offsets and out are device (HBM) pointers */
+#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); staged through pinned buffers */
+
+/* One result record: identical bytes to SHF_HASH (shf.private.h:180-185). */
+typedef struct shf_hash128 {
+    uint64_t h1; /* SHF_HASH.u64[0] */
+    uint64_t h2; /* SHF_HASH.u64[1] */
+} shf_hash128;
+
+/* The hash bits put/find consume (shf.c:800-803, :893-896), packed in one u64:
+ *   bits  0.. 7 win  = SHF_HASH.u16[0] % 256
+ *   bits  8..18 tab  = SHF_HASH.u16[1] % 2048
+ *   bits 19..27 row  = SHF_HASH.u16[2] % 512
+ *   bits 28..31 0    (the SHF_UID `ref` field, chosen later by put)
+ *   bits 32..52 rnd  = SHF_HASH.u32[2] % 2^21
+ * i.e. the low word is SHF_UID.as_u32 (shf.private.h:170-178) with ref = 0. */
+#define SHF_UID_PARTS_WIN(p) ((uint32_t)((p)&0xffu))
+#define SHF_UID_PARTS_TAB(p) ((uint32_t)(((p) >> 8) & 0x7ffu))
+#define SHF_UID_PARTS_ROW(p) ((uint32_t)(((p) >> 19) & 0x1ffu))
+#define SHF_UID_PARTS_RND(p) ((uint32_t)(((p) >> 32) & 0x1fffffu))
+
+/* ---- fixed-length keys: key i = keys[i*key_len .. (i+1)*key_len) ---------- */
+
+/* Synchronous. mem = SHF_HASH_MEM_DEVICE or SHF_HASH_MEM_HOST; out = n records. */
+SHF_HB_API int shf_hash_batch_fixed(const void *keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                         shf_hash128 *out, int mem);
+
+/* Asynchronous, device-resident: enqueue on `hip_stream` (NULL = the null
+ * stream) and return; results are valid once that stream has reached the
+ * point of the call. */
+SHF_HB_API int shf_hash_batch_fixed_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                               shf_hash128 *d_out, void *hip_stream);
+
+/* ---- variable-length keys: key i = bytes[offsets[i] .. offsets[i+1]) ------- */
+/* offsets has n + 1 monotone entries (64-bit, so batches may exceed 4 GiB). */
+
+SHF_HB_API int shf_hash_batch_var(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
+                       shf_hash128 *out, int mem);
+
+SHF_HB_API int shf_hash_batch_var_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n, uint32_t seed,
+                             shf_hash128 *d_out, void *hip_stream);
+
+/* ---- UID parts instead of the 16-byte hash (8 B per key, see above) ------- */
+
+SHF_HB_API int shf_uid_parts_batch_fixed_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                    uint64_t *d_parts, void *hip_stream);
+SHF_HB_API int shf_uid_parts_batch_var_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n, uint32_t seed,
+                                  uint64_t *d_parts, void *hip_stream);
+
+/* ---- several GPUs: host buffers in and out, keys split into n_devices even
+ * index ranges, one host thread and one device per range, no collective.
+ * n_devices <= 0 means every visible device. ------------------------------ */
+
+SHF_HB_API int shf_hash_batch_fixed_multi(const void *keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                               shf_hash128 *out, int n_devices);
+SHF_HB_API int shf_hash_batch_var_multi(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
+                             shf_hash128 *out, int n_devices);
+
+/* ---- kernel selection (tests and benchmarks) ------------------------------- */
+#define SHF_HB_KERNEL_AUTO 0    /* what every function above uses */
+#define SHF_HB_KERNEL_FIXED16 1 /* key_len == 16, 16-B aligned keys */
+#define SHF_HB_KERNEL_TILED 2   /* key_len % 16 == 0, >= 32, 16-B aligned keys */
+#define SHF_HB_KERNEL_GENERIC 3 /* any key_len, any alignment */
+
+SHF_HB_API int shf_hash_batch_fixed_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                      shf_hash128 *d_out, int kernel, void *hip_stream);
+
+/* ---- info ----------------------------------------------------------------- */
+SHF_HB_API int shf_hash_batch_device_count(void);          /* visible HIP devices, or a negative status */
+SHF_HB_API int shf_hash_batch_check_device(void);          /* SHF_HB_OK if the current device can run the kernels */
+SHF_HB_API int shf_hash_batch_last_hip_error(void);        /* last hipError_t seen by this thread */
+SHF_HB_API const char *shf_hash_batch_strerror(int status);
+SHF_HB_API const char *shf_hash_batch_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHF_HASH_BATCH_H */

@@ -1,0 +1,257 @@
+"""MI355X batch key hashing for SharedHashFile (Python side of the C ABI).
+
+The product is the C-ABI library ``libshf_hash_batch.so`` (include/shf_hash_batch.h).
+This module only binds it with ctypes so the tests and bench.py can drive it with
+torch device buffers or numpy host buffers. It mirrors the reference seam:
+
+    shf_make_hash(key, key_len)            /root/reference/src/shf.c:450-462
+      -> SHF_HASH {u64[0]=h1, u64[1]=h2}   /root/reference/src/shf.private.h:180-185
+
+for a whole batch: results are (n, 2) uint64 arrays, row i = SHF_HASH of key i.
+
+There is no CPU fallback. If the library is missing or cannot run on the device,
+every call raises ShfHashBatchError / RuntimeError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+SEED = 12345  # src/shf.c:456
+
+OK = 0
+ERR_ARG = -1
+ERR_NODEV = -2
+ERR_HIP = -3
+ERR_NOMEM = -4
+ERR_ARCH = -5
+
+MEM_DEVICE = 0
+MEM_HOST = 1
+
+KERNEL_AUTO = 0
+KERNEL_FIXED16 = 1
+KERNEL_TILED = 2
+KERNEL_GENERIC = 3
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libshf_hash_batch.so")
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "shf_hash_batch.h")
+
+_lib = None
+
+
+class ShfHashBatchError(RuntimeError):
+    def __init__(self, status, where, hip_error=0):
+        self.status = status
+        self.hip_error = hip_error
+        msg = "%s failed: %s (status %d" % (where, _strerror(status), status)
+        if hip_error:
+            msg += ", hipError %d" % hip_error
+        super().__init__(msg + ")")
+
+
+def _strerror(status):
+    try:
+        return load().shf_hash_batch_strerror(status).decode()
+    except Exception:  # pragma: no cover - only when the library itself is broken
+        return "status %d" % status
+
+
+_VP = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_INT = ctypes.c_int
+
+_SIGS = {
+    "shf_hash_batch_fixed": [_VP, _U32, _U64, _U32, _VP, _INT],
+    "shf_hash_batch_fixed_async": [_VP, _U32, _U64, _U32, _VP, _VP],
+    "shf_hash_batch_var": [_VP, _VP, _U64, _U32, _VP, _INT],
+    "shf_hash_batch_var_async": [_VP, _VP, _U64, _U32, _VP, _VP],
+    "shf_uid_parts_batch_fixed_async": [_VP, _U32, _U64, _U32, _VP, _VP],
+    "shf_uid_parts_batch_var_async": [_VP, _VP, _U64, _U32, _VP, _VP],
+    "shf_hash_batch_fixed_multi": [_VP, _U32, _U64, _U32, _VP, _INT],
+    "shf_hash_batch_var_multi": [_VP, _VP, _U64, _U32, _VP, _INT],
+    "shf_hash_batch_fixed_kernel_async": [_VP, _U32, _U64, _U32, _VP, _INT, _VP],
+    "shf_hash_batch_device_count": [],
+    "shf_hash_batch_check_device": [],
+    "shf_hash_batch_last_hip_error": [],
+    "shf_hash_batch_strerror": [_INT],
+    "shf_hash_batch_version": [],
+}
+
+
+def load(path=None):
+    """Load the C-ABI library (raises loudly when it is not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError("libshf_hash_batch.so not built (%s); run python -m sharedhashfile_amd.build" % p)
+    lib = ctypes.CDLL(p)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_char_p if name in ("shf_hash_batch_strerror", "shf_hash_batch_version") else ctypes.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def header_functions(header=HEADER_PATH):
+    """Names of every function include/shf_hash_batch.h declares."""
+    import re
+
+    txt = open(header).read()
+    return sorted(set(re.findall(r"SHF_HB_API\s+(?:const\s+char\s*\*|int)\s*(shf_\w+)\s*\(", txt)))
+
+
+def _check(rc, where):
+    if rc != OK:
+        raise ShfHashBatchError(rc, where, load().shf_hash_batch_last_hip_error())
+
+
+# ---------------------------------------------------------------------------
+# torch device-resident helpers (pointers are HBM addresses)
+# ---------------------------------------------------------------------------
+def _stream_handle(stream):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _require_cuda_u8(t, name):
+    import torch
+
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise TypeError("%s must be a CUDA (HIP) tensor" % name)
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+
+
+def hash_fixed(keys, key_len=None, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO):
+    """Hash n fixed-length keys resident on the GPU.
+
+    keys: uint8 CUDA tensor (n, key_len) or flat with key_len given.
+    Returns an int64 CUDA tensor (n, 2) holding the uint64 bit patterns of
+    (h1, h2) = SHF_HASH.u64[0..1] per key. Asynchronous on `stream`.
+    """
+    import torch
+
+    _require_cuda_u8(keys, "keys")
+    if key_len is None:
+        if keys.dim() != 2:
+            raise ValueError("pass key_len for a flat key buffer")
+        n, key_len = keys.shape
+    else:
+        n = keys.numel() // key_len if key_len else 0
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=keys.device)
+    rc = load().shf_hash_batch_fixed_kernel_async(
+        ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()), kernel,
+        _stream_handle(stream))
+    _check(rc, "shf_hash_batch_fixed_kernel_async")
+    return out
+
+
+def hash_var(data, offsets, seed=SEED, out=None, stream=None):
+    """Hash n variable-length keys on the GPU: key i = data[offsets[i]:offsets[i+1]].
+
+    data: uint8 CUDA tensor; offsets: int64 CUDA tensor of n + 1 entries.
+    """
+    import torch
+
+    _require_cuda_u8(data, "data")
+    n = offsets.numel() - 1
+    if out is None:
+        out = torch.empty((max(n, 0), 2), dtype=torch.int64, device=data.device)
+    rc = load().shf_hash_batch_var_async(
+        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
+        ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _check(rc, "shf_hash_batch_var_async")
+    return out
+
+
+def uid_parts_fixed(keys, key_len=None, seed=SEED, out=None, stream=None):
+    """Packed win/tab/row/rnd (include/shf_hash_batch.h SHF_UID_PARTS_*) per key."""
+    import torch
+
+    _require_cuda_u8(keys, "keys")
+    if key_len is None:
+        n, key_len = keys.shape
+    else:
+        n = keys.numel() // key_len if key_len else 0
+    if out is None:
+        out = torch.empty((n,), dtype=torch.int64, device=keys.device)
+    rc = load().shf_uid_parts_batch_fixed_async(
+        ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _check(rc, "shf_uid_parts_batch_fixed_async")
+    return out
+
+
+def uid_parts_var(data, offsets, seed=SEED, out=None, stream=None):
+    import torch
+
+    _require_cuda_u8(data, "data")
+    n = offsets.numel() - 1
+    if out is None:
+        out = torch.empty((max(n, 0),), dtype=torch.int64, device=data.device)
+    rc = load().shf_uid_parts_batch_var_async(
+        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
+        ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _check(rc, "shf_uid_parts_batch_var_async")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# numpy host-memory helpers (library stages through pinned buffers)
+# ---------------------------------------------------------------------------
+def _np_u8(a):
+    a = np.ascontiguousarray(a)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8)
+    return a
+
+
+def hash_fixed_host(keys, key_len=None, seed=SEED, n_devices=None):
+    """Host buffers in, host (n, 2) uint64 out. n_devices: None = current device only."""
+    keys = _np_u8(keys)
+    if key_len is None:
+        n, key_len = keys.shape
+    else:
+        n = keys.size // key_len if key_len else 0
+    out = np.empty((n, 2), dtype=np.uint64)
+    lib = load()
+    if n_devices is None:
+        rc = lib.shf_hash_batch_fixed(keys.ctypes.data, key_len, n, seed, out.ctypes.data, MEM_HOST)
+        _check(rc, "shf_hash_batch_fixed")
+    else:
+        rc = lib.shf_hash_batch_fixed_multi(keys.ctypes.data, key_len, n, seed, out.ctypes.data, n_devices)
+        _check(rc, "shf_hash_batch_fixed_multi")
+    return out
+
+
+def hash_var_host(data, offsets, seed=SEED, n_devices=None):
+    data = _np_u8(data)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    out = np.empty((max(n, 0), 2), dtype=np.uint64)
+    lib = load()
+    if n_devices is None:
+        rc = lib.shf_hash_batch_var(data.ctypes.data, offsets.ctypes.data, max(n, 0), seed, out.ctypes.data, MEM_HOST)
+        _check(rc, "shf_hash_batch_var")
+    else:
+        rc = lib.shf_hash_batch_var_multi(data.ctypes.data, offsets.ctypes.data, max(n, 0), seed, out.ctypes.data,
+                                          n_devices)
+        _check(rc, "shf_hash_batch_var_multi")
+    return out
+
+
+def device_count():
+    return load().shf_hash_batch_device_count()
+
+
+def check_device():
+    _check(load().shf_hash_batch_check_device(), "shf_hash_batch_check_device")

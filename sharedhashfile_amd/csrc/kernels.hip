@@ -1,0 +1,305 @@
+// Batch key-hashing kernels for MI355X (gfx950).
+//
+// Each kernel computes, for every key of a batch, exactly what the reference's
+// shf_make_hash() leaves in the thread-local SHF_HASH
+// (/root/reference/src/shf.c:450-462 -> murmurhash3.c:75-160), or the packed
+// UID parts that put/find derive from it (shf.c:800-803, :893-896).
+//
+// Kernels (see DESIGN.md for the roofline of each):
+//   k_fixed16   key_len == 16: one lane per key, one 16-B coalesced load and one
+//               16-B coalesced store per lane. HBM-bound (32 B/key).
+//   k_tiled     key_len % 16 == 0, key_len >= 32 (the 256-B config): a wave owns
+//               64 keys; every round it stages 128 B of each key through LDS with
+//               fully-used 128-B segment loads, XOR-swizzled so the lane-per-key
+//               ds_read_b128 reads are bank-conflict free, and prefetches the next
+//               round into registers while hashing the current one.
+//   k_generic   any length, fixed or variable (offset array): one lane per key,
+//               64-B per-lane bursts of dword-aligned loads, funnel-shifted with
+//               v_alignbyte_b32 for unaligned key starts.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "murmur3_mix.h"
+#include "kernels.h"
+
+namespace shfhb {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int OUT>
+__device__ __forceinline__ void store_result(void* __restrict__ out, uint64_t i, const State& s) {
+  if constexpr (OUT == kOutHash) {
+    u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
+    reinterpret_cast<u32x4*>(out)[i] = v;
+  } else {
+    reinterpret_cast<uint64_t*>(out)[i] = uid_parts(s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// key_len == 16
+// ---------------------------------------------------------------------------
+template <int OUT>
+__global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
+                                                 void* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u32x4 k = __builtin_nontemporal_load(&keys[i]);
+    State s{seed, seed};
+    body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
+    finish(s, 16);
+    store_result<OUT>(out, i, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic: one lane per key, any alignment, any length.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t low_bytes_mask(uint32_t nbytes) {
+  return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1ull);
+}
+
+// Hash `len` bytes at `p` (any alignment). Only dwords that hold at least one
+// byte of the key are ever loaded, so no access can cross into an unmapped page.
+__device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint32_t seed) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+  const uint32_t sh = (uint32_t)(addr & 3u);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(addr - sh);
+  const uint32_t nblocks = len >> 4;
+  State s{seed, seed};
+
+  uint32_t j = 0;
+  for (; j + 4 <= nblocks; j += 4) {  // 64-B burst per lane
+    const u32x4_a4* v = reinterpret_cast<const u32x4_a4*>(w + 4 * j);
+    const u32x4 a = v[0], b = v[1], c = v[2], d = v[3];
+    const uint32_t e = sh ? w[4 * j + 16] : 0u;
+    const uint32_t x[17] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d0 = __builtin_amdgcn_alignbyte(x[4 * q + 1], x[4 * q + 0], sh);
+      const uint32_t d1 = __builtin_amdgcn_alignbyte(x[4 * q + 2], x[4 * q + 1], sh);
+      const uint32_t d2 = __builtin_amdgcn_alignbyte(x[4 * q + 3], x[4 * q + 2], sh);
+      const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4 * q + 4], x[4 * q + 3], sh);
+      body_block(s, pack64(d0, d1), pack64(d2, d3));
+    }
+  }
+  for (; j < nblocks; ++j) {
+    const u32x4 a = *reinterpret_cast<const u32x4_a4*>(w + 4 * j);
+    const uint32_t e = sh ? w[4 * j + 4] : 0u;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(a.w, a.z, sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(e, a.w, sh);
+    body_block(s, pack64(d0, d1), pack64(d2, d3));
+  }
+
+  const uint32_t rem = len & 15u;
+  if (rem) {
+    const uint32_t* t = w + 4 * nblocks;
+    const uint32_t need = sh + rem;  // bytes spanned from the aligned base
+    uint32_t x[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) x[q] = (4u * q < need) ? t[q] : 0u;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
+    const uint64_t t1 = pack64(d0, d1) & low_bytes_mask(rem);
+    const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
+    tail_block(s, t1, t2, rem);
+  }
+  finish(s, len);
+  return s;
+}
+
+template <int OUT, bool VAR>
+__global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ bytes,
+                                                 const uint64_t* __restrict__ offsets, uint64_t off_base,
+                                                 uint32_t key_len, uint64_t n, uint32_t seed,
+                                                 void* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t start;
+    uint32_t len;
+    if constexpr (VAR) {
+      const uint64_t o0 = offsets[i], o1 = offsets[i + 1];
+      start = o0 - off_base;
+      len = (uint32_t)(o1 - o0);
+    } else {
+      start = i * (uint64_t)key_len;
+      len = key_len;
+    }
+    const State s = hash_bytes(bytes + start, len, seed);
+    store_result<OUT>(out, i, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tiled: key_len % 16 == 0 and key_len >= 32. One wave = 64 keys; each round
+// moves 8 blocks (128 B) of every key through an 8-KiB LDS tile per wave.
+//
+// Load mapping (round r, instruction q = 0..7): lane l fetches 16 B of key
+// 8q + l/8 at byte 128r + 16(l%8): 8 lanes read one contiguous 128-B segment.
+// LDS layout: key k's piece j sits at k*128 + 16*(j ^ ((k >> 1) & 7)). Writes
+// (8 lanes per row) cover a row's 32 banks once; the lane-per-key reads of one
+// piece index hit 16 distinct (k&1, slot) pairs per ds_read_b128 lane group, so
+// both sides are conflict free.
+// ---------------------------------------------------------------------------
+constexpr int kTileKeys = 64;
+constexpr int kRoundBlocks = 8;
+constexpr int kTiledWaves = 4;  // waves per workgroup
+
+__device__ __forceinline__ uint32_t tile_slot(uint32_t key, uint32_t piece) {
+  return key * (kRoundBlocks * 16) + 16u * (piece ^ ((key >> 1) & 7u));
+}
+
+template <int OUT>
+__global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __restrict__ keys, uint32_t key_len,
+                                                            uint64_t n, uint32_t seed, void* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kTiledWaves][kTileKeys * kRoundBlocks * 16];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;
+  uint8_t* tile = lds[wave];
+
+  const uint32_t nblocks = key_len >> 4;
+  const uint32_t rounds = (nblocks + kRoundBlocks - 1) / kRoundBlocks;
+  const uint64_t ntiles = (n + kTileKeys - 1) / kTileKeys;
+  const uint64_t wstride = (uint64_t)gridDim.x * kTiledWaves;
+  uint64_t t = (uint64_t)blockIdx.x * kTiledWaves + wave;
+  if (t >= ntiles) return;
+
+  const uint32_t ld_key_sub = lane >> 3;  // + 8q
+  const uint32_t ld_piece = lane & 7u;
+
+  // Fetch round r of tile t into registers (8 x 16 B per lane).
+  auto fetch = [&](uint64_t tt, uint32_t r, u32x4 (&reg)[kRoundBlocks]) {
+    const uint64_t k0 = tt * kTileKeys;
+    const uint32_t rb = min((uint32_t)kRoundBlocks, nblocks - r * kRoundBlocks);
+#pragma unroll
+    for (int q = 0; q < kRoundBlocks; ++q) {
+      const uint64_t key = k0 + 8u * q + ld_key_sub;
+      if (key < n && ld_piece < rb) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(keys + key * key_len + (uint64_t)r * 128u + 16u * ld_piece);
+        reg[q] = __builtin_nontemporal_load(src);
+      } else {
+        reg[q] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+
+  u32x4 nxt[kRoundBlocks];
+  fetch(t, 0, nxt);
+  uint32_t r = 0;
+  State s{seed, seed};
+  while (true) {
+    // Stage the fetched round into LDS.
+#pragma unroll
+    for (int q = 0; q < kRoundBlocks; ++q)
+      *reinterpret_cast<u32x4*>(tile + tile_slot(8u * q + ld_key_sub, ld_piece)) = nxt[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // Prefetch the next round (or the next tile's first round).
+    const uint32_t rb = min((uint32_t)kRoundBlocks, nblocks - r * kRoundBlocks);
+    uint64_t t_next = t;
+    uint32_t r_next = r + 1;
+    if (r_next == rounds) {
+      t_next = t + wstride;
+      r_next = 0;
+    }
+    const bool more = t_next < ntiles;
+    if (more) fetch(t_next, r_next, nxt);
+
+    // Hash this round's blocks of this lane's key.
+#pragma unroll
+    for (int j = 0; j < kRoundBlocks; ++j) {
+      if ((uint32_t)j < rb) {
+        const u32x4 b = *reinterpret_cast<const u32x4*>(tile + tile_slot(lane, (uint32_t)j));
+        body_block(s, pack64(b.x, b.y), pack64(b.z, b.w));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    if (r + 1 == rounds) {
+      const uint64_t key = t * kTileKeys + lane;
+      finish(s, key_len);
+      if (key < n) store_result<OUT>(out, key, s);
+      s = State{seed, seed};
+    }
+    if (!more) break;
+    t = t_next;
+    r = r_next;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
+  uint64_t g = (items + per_block - 1) / per_block;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  return (unsigned)g;
+}
+
+template <int OUT>
+static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out,
+                                 hipStream_t st, int kernel) {
+  const unsigned cap = 256u * 32u;  // 256 CUs x 8 blocks x 4 waves of grid-stride
+  if (kernel == kKernelAuto) {
+    if (key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0) kernel = kKernelFixed16;
+    else if (key_len >= 32 && (key_len & 15u) == 0 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0)
+      kernel = kKernelTiled;
+    else kernel = kKernelGeneric;
+  }
+  switch (kernel) {
+    case kKernelFixed16:
+      if (key_len != 16 || (reinterpret_cast<uintptr_t>(keys) & 15u)) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(k_fixed16<OUT>, dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+                         reinterpret_cast<const u32x4*>(keys), n, seed, out);
+      break;
+    case kKernelTiled: {
+      if (key_len < 16 || (key_len & 15u) || (reinterpret_cast<uintptr_t>(keys) & 15u)) return hipErrorInvalidValue;
+      const uint64_t tiles = (n + kTileKeys - 1) / kTileKeys;
+      hipLaunchKernelGGL(k_tiled<OUT>, dim3(grid_for(tiles, kTiledWaves, 256u * 8u)), dim3(64 * kTiledWaves), 0, st,
+                         reinterpret_cast<const uint8_t*>(keys), key_len, n, seed, out);
+      break;
+    }
+    default:
+      hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+                         reinterpret_cast<const uint8_t*>(keys), (const uint64_t*)nullptr, (uint64_t)0, key_len, n,
+                         seed, out);
+      break;
+  }
+  return hipGetLastError();
+}
+
+template <int OUT>
+static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
+                               uint32_t seed, void* out, hipStream_t st) {
+  const unsigned cap = 256u * 32u;
+  hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out, int out_mode,
+                        hipStream_t st, int kernel) {
+  if (n == 0) return hipSuccess;
+  return out_mode == kOutHash ? launch_fixed_t<kOutHash>(keys, key_len, n, seed, out, st, kernel)
+                              : launch_fixed_t<kOutUid>(keys, key_len, n, seed, out, st, kernel);
+}
+
+hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
+                      void* out, int out_mode, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  return out_mode == kOutHash ? launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, out, st)
+                              : launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, out, st);
+}
+
+}  // namespace shfhb

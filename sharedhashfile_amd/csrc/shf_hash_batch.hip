@@ -1,0 +1,435 @@
+// C-ABI host layer of the MI355X batch key-hashing stage (include/shf_hash_batch.h).
+//
+// Replaces, for batches, the per-key seam shf_make_hash() (/root/reference/src/shf.c:450-462):
+// same 16 output bytes per key (SHF_HASH layout, shf.private.h:180-185), computed by the
+// kernels in kernels.hip. This file owns: argument checking, per-thread/per-device HIP
+// contexts (streams + staging buffers), the host-memory pipeline (pinned double-buffered
+// chunks, H2D / kernel / D2H overlapped on two streams) and the multi-GPU split.
+// There is deliberately no CPU path: without a gfx950 device every call fails loudly.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <thread>
+#include <vector>
+
+#include "../../include/shf_hash_batch.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local int tls_last_hip = 0;
+
+int map_hip(hipError_t e) {
+  if (e == hipSuccess) return SHF_HB_OK;
+  tls_last_hip = (int)e;
+  switch (e) {
+    case hipErrorOutOfMemory:
+      return SHF_HB_ERR_NOMEM;
+    case hipErrorNoDevice:
+    case hipErrorInsufficientDriver:
+    case hipErrorInvalidDevice:
+      return SHF_HB_ERR_NODEV;
+    case hipErrorNoBinaryForGpu:
+      return SHF_HB_ERR_ARCH;
+    default:
+      return SHF_HB_ERR_HIP;
+  }
+}
+
+#define HB_TRY(expr)                       \
+  do {                                     \
+    hipError_t e_ = (expr);                \
+    if (e_ != hipSuccess) return map_hip(e_); \
+  } while (0)
+
+constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `const int len`
+constexpr size_t kStageBytes = (size_t)64 << 20;   // key bytes per pipeline chunk
+constexpr int kSlots = 2;                          // double buffering
+
+// Per (thread, device) resources. Created lazily, reused across calls.
+struct DevCtx {
+  int dev = -1;
+  int status = SHF_HB_OK;
+  hipStream_t st[kSlots] = {nullptr, nullptr};
+  hipEvent_t done[kSlots] = {nullptr, nullptr};
+  uint8_t* h_in[kSlots] = {nullptr, nullptr};
+  uint8_t* d_in[kSlots] = {nullptr, nullptr};
+  size_t in_cap = 0;
+  shf_hash128* h_out[kSlots] = {nullptr, nullptr};
+  shf_hash128* d_out[kSlots] = {nullptr, nullptr};
+  uint64_t* h_off[kSlots] = {nullptr, nullptr};
+  uint64_t* d_off[kSlots] = {nullptr, nullptr};
+  size_t key_cap = 0;  // records in h_out/d_out and offsets (+1) per slot
+};
+
+thread_local std::map<int, DevCtx*> tls_ctx;
+
+int check_arch(int dev) {
+  hipDeviceProp_t p;
+  HB_TRY(hipGetDeviceProperties(&p, dev));
+  if (strncmp(p.gcnArchName, "gfx950", 6) != 0) return SHF_HB_ERR_ARCH;
+  return SHF_HB_OK;
+}
+
+int current_ctx(DevCtx** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return map_hip(e) == SHF_HB_ERR_HIP ? SHF_HB_ERR_NODEV : map_hip(e);
+  }
+  auto it = tls_ctx.find(dev);
+  if (it != tls_ctx.end()) {
+    *out = it->second;
+    return it->second->status;
+  }
+  DevCtx* c = new DevCtx();
+  c->dev = dev;
+  c->status = check_arch(dev);
+  if (c->status == SHF_HB_OK) {
+    for (int s = 0; s < kSlots && c->status == SHF_HB_OK; ++s) {
+      c->status = map_hip(hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking));
+      if (c->status == SHF_HB_OK) c->status = map_hip(hipEventCreateWithFlags(&c->done[s], hipEventDisableTiming));
+    }
+  }
+  tls_ctx[dev] = c;
+  *out = c;
+  return c->status;
+}
+
+void free_staging(DevCtx* c) {
+  for (int s = 0; s < kSlots; ++s) {
+    if (c->h_in[s]) (void)hipHostFree(c->h_in[s]);
+    if (c->d_in[s]) (void)hipFree(c->d_in[s]);
+    if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
+    if (c->d_out[s]) (void)hipFree(c->d_out[s]);
+    if (c->h_off[s]) (void)hipHostFree(c->h_off[s]);
+    if (c->d_off[s]) (void)hipFree(c->d_off[s]);
+    c->h_in[s] = c->d_in[s] = nullptr;
+    c->h_out[s] = c->d_out[s] = nullptr;
+    c->h_off[s] = c->d_off[s] = nullptr;
+  }
+  c->in_cap = c->key_cap = 0;
+}
+
+// Release every context of this thread (worker threads of the *_multi calls).
+void release_thread_ctx() {
+  for (auto& kv : tls_ctx) {
+    DevCtx* c = kv.second;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->dev);
+    for (int s = 0; s < kSlots; ++s) {
+      if (c->st[s]) (void)hipStreamSynchronize(c->st[s]);
+    }
+    free_staging(c);
+    for (int s = 0; s < kSlots; ++s) {
+      if (c->done[s]) (void)hipEventDestroy(c->done[s]);
+      if (c->st[s]) (void)hipStreamDestroy(c->st[s]);
+    }
+    (void)hipSetDevice(prev);
+    delete c;
+  }
+  tls_ctx.clear();
+}
+
+int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys) {
+  if (in_bytes <= c->in_cap && keys <= c->key_cap) return SHF_HB_OK;
+  for (int s = 0; s < kSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
+  const size_t ib = std::max(in_bytes, c->in_cap), kc = std::max(keys, c->key_cap);
+  free_staging(c);
+  for (int s = 0; s < kSlots; ++s) {
+    HB_TRY(hipHostMalloc((void**)&c->h_in[s], ib, hipHostMallocDefault));
+    HB_TRY(hipMalloc((void**)&c->d_in[s], ib));
+    HB_TRY(hipHostMalloc((void**)&c->h_out[s], kc * sizeof(shf_hash128), hipHostMallocDefault));
+    HB_TRY(hipMalloc((void**)&c->d_out[s], kc * sizeof(shf_hash128)));
+    HB_TRY(hipHostMalloc((void**)&c->h_off[s], (kc + 1) * sizeof(uint64_t), hipHostMallocDefault));
+    HB_TRY(hipMalloc((void**)&c->d_off[s], (kc + 1) * sizeof(uint64_t)));
+  }
+  c->in_cap = ib;
+  c->key_cap = kc;
+  return SHF_HB_OK;
+}
+
+// One chunk in flight per slot; `pending` remembers where its results go.
+struct Pending {
+  bool busy = false;
+  shf_hash128* dst = nullptr;
+  uint64_t count = 0;
+};
+
+int drain_slot(DevCtx* c, int s, Pending& p) {
+  if (!p.busy) return SHF_HB_OK;
+  HB_TRY(hipEventSynchronize(c->done[s]));
+  memcpy(p.dst, c->h_out[s], p.count * sizeof(shf_hash128));
+  p.busy = false;
+  return SHF_HB_OK;
+}
+
+// Host-memory fixed-length pipeline on the current device.
+int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out) {
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  const uint64_t per = key_len ? std::max<uint64_t>(1, kStageBytes / key_len) : (uint64_t)1 << 22;
+  const uint64_t chunk = std::min<uint64_t>(per, n);
+  if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk))) return rc;
+  Pending pend[kSlots];
+  uint64_t idx = 0;
+  for (uint64_t i0 = 0; i0 < n; i0 += chunk, ++idx) {
+    const int s = (int)(idx % kSlots);
+    if ((rc = drain_slot(c, s, pend[s]))) return rc;
+    const uint64_t cnt = std::min(chunk, n - i0);
+    const size_t nb = (size_t)cnt * key_len;
+    if (nb) memcpy(c->h_in[s], keys + i0 * key_len, nb);
+    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], c->h_in[s], nb, hipMemcpyHostToDevice, c->st[s]));
+    HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, c->d_out[s], shfhb::kOutHash, c->st[s],
+                               shfhb::kKernelAuto));
+    HB_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128), hipMemcpyDeviceToHost, c->st[s]));
+    HB_TRY(hipEventRecord(c->done[s], c->st[s]));
+    pend[s] = Pending{true, out + i0, cnt};
+  }
+  for (int s = 0; s < kSlots; ++s)
+    if ((rc = drain_slot(c, s, pend[s]))) return rc;
+  return SHF_HB_OK;
+}
+
+// Host-memory variable-length pipeline: chunks of whole keys up to kStageBytes
+// of key bytes (a single larger key gets a chunk of its own).
+int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  const uint64_t max_keys = std::min<uint64_t>(n, (uint64_t)1 << 22);
+  Pending pend[kSlots];
+  uint64_t idx = 0;
+  for (uint64_t i0 = 0; i0 < n; ++idx) {
+    // extend the chunk while it fits the byte budget and key budget
+    uint64_t i1 = i0 + 1;
+    const uint64_t base = offsets[i0];
+    {
+      uint64_t lo = i1, hi = std::min(n, i0 + max_keys);
+      // largest i1 in [i0+1, hi] with offsets[i1] - base <= kStageBytes (offsets monotone)
+      while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo + 1) / 2;
+        if (offsets[mid] - base <= kStageBytes) lo = mid;
+        else hi = mid - 1;
+      }
+      i1 = lo;
+    }
+    const uint64_t cnt = i1 - i0;
+    const size_t nb = (size_t)(offsets[i1] - base);
+    if ((rc = ensure_staging(c, std::max(nb, (size_t)1), (size_t)std::max<uint64_t>(cnt, max_keys)))) return rc;
+    const int s = (int)(idx % kSlots);
+    if ((rc = drain_slot(c, s, pend[s]))) return rc;
+    if (nb) memcpy(c->h_in[s], bytes + base, nb);
+    memcpy(c->h_off[s], offsets + i0, (cnt + 1) * sizeof(uint64_t));
+    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], c->h_in[s], nb, hipMemcpyHostToDevice, c->st[s]));
+    HB_TRY(hipMemcpyAsync(c->d_off[s], c->h_off[s], (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
+    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, c->d_out[s], shfhb::kOutHash, c->st[s]));
+    HB_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128), hipMemcpyDeviceToHost, c->st[s]));
+    HB_TRY(hipEventRecord(c->done[s], c->st[s]));
+    pend[s] = Pending{true, out + i0, cnt};
+    i0 = i1;
+  }
+  for (int s = 0; s < kSlots; ++s)
+    if ((rc = drain_slot(c, s, pend[s]))) return rc;
+  return SHF_HB_OK;
+}
+
+int check_var_lengths_host(const uint64_t* offsets, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  }
+  return SHF_HB_OK;
+}
+
+int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out, int out_mode,
+                 hipStream_t st, int kernel, bool sync) {
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  if (sync) st = c->st[0];
+  HB_TRY(shfhb::launch_fixed(keys, key_len, n, seed, out, out_mode, st, kernel));
+  if (sync) HB_TRY(hipStreamSynchronize(st));
+  return SHF_HB_OK;
+}
+
+int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, void* out, int out_mode,
+               hipStream_t st, bool sync) {
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  if (sync) st = c->st[0];
+  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, out, out_mode, st));
+  if (sync) HB_TRY(hipStreamSynchronize(st));
+  return SHF_HB_OK;
+}
+
+int visible_devices() {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return SHF_HB_ERR_NODEV;
+  }
+  return n;
+}
+
+template <class F>
+int run_multi(uint64_t n, int n_devices, F&& shard_fn) {
+  const int vis = visible_devices();
+  if (vis < 0) return vis;
+  if (vis == 0) return SHF_HB_ERR_NODEV;
+  int g = n_devices <= 0 ? vis : std::min(n_devices, vis);
+  if ((uint64_t)g > n) g = (int)std::max<uint64_t>(1, n);
+  std::vector<int> rcs(g, SHF_HB_OK);
+  std::vector<int> errs(g, 0);
+  std::vector<std::thread> th;
+  for (int d = 0; d < g; ++d) {
+    const uint64_t lo = n * (uint64_t)d / (uint64_t)g, hi = n * (uint64_t)(d + 1) / (uint64_t)g;
+    th.emplace_back([&, d, lo, hi]() {
+      hipError_t e = hipSetDevice(d);
+      if (e != hipSuccess) {
+        rcs[d] = map_hip(e);
+      } else if (hi > lo) {
+        rcs[d] = shard_fn(lo, hi);
+      }
+      errs[d] = tls_last_hip;
+      release_thread_ctx();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int d = 0; d < g; ++d) {
+    if (rcs[d] != SHF_HB_OK) {
+      tls_last_hip = errs[d];
+      return rcs[d];
+    }
+  }
+  return SHF_HB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shf_hash_batch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
+                         int mem) {
+  if (n == 0) return SHF_HB_OK;
+  if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  if (mem == SHF_HASH_MEM_DEVICE)
+    return device_fixed(keys, key_len, n, seed, out, shfhb::kOutHash, nullptr, shfhb::kKernelAuto, true);
+  if (mem == SHF_HASH_MEM_HOST) return host_fixed((const uint8_t*)keys, key_len, n, seed, out);
+  return SHF_HB_ERR_ARG;
+}
+
+int shf_hash_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* d_out,
+                               void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  return device_fixed(d_keys, key_len, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream,
+                      shfhb::kKernelAuto, false);
+}
+
+int shf_hash_batch_fixed_kernel_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                      shf_hash128* d_out, int kernel, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  if (kernel < SHF_HB_KERNEL_AUTO || kernel > SHF_HB_KERNEL_GENERIC) return SHF_HB_ERR_ARG;
+  if (kernel == SHF_HB_KERNEL_FIXED16 && (key_len != 16 || ((uintptr_t)d_keys & 15u))) return SHF_HB_ERR_ARG;
+  if (kernel == SHF_HB_KERNEL_TILED && (key_len < 32 || (key_len & 15u) || ((uintptr_t)d_keys & 15u)))
+    return SHF_HB_ERR_ARG;
+  return device_fixed(d_keys, key_len, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, kernel, false);
+}
+
+int shf_hash_batch_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out,
+                       int mem) {
+  if (n == 0) return SHF_HB_OK;
+  if (!out || !offsets || !bytes) return SHF_HB_ERR_ARG;
+  if (mem == SHF_HASH_MEM_DEVICE) return device_var(bytes, offsets, n, seed, out, shfhb::kOutHash, nullptr, true);
+  if (mem == SHF_HASH_MEM_HOST) {
+    int rc = check_var_lengths_host(offsets, n);
+    if (rc) return rc;
+    return host_var((const uint8_t*)bytes, offsets, n, seed, out);
+  }
+  return SHF_HB_ERR_ARG;
+}
+
+int shf_hash_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
+                             shf_hash128* d_out, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
+  return device_var(d_bytes, d_offsets, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, false);
+}
+
+int shf_uid_parts_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                    uint64_t* d_parts, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_parts || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  return device_fixed(d_keys, key_len, n, seed, d_parts, shfhb::kOutUid, (hipStream_t)hip_stream,
+                      shfhb::kKernelAuto, false);
+}
+
+int shf_uid_parts_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
+                                  uint64_t* d_parts, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_parts || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
+  return device_var(d_bytes, d_offsets, n, seed, d_parts, shfhb::kOutUid, (hipStream_t)hip_stream, false);
+}
+
+int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
+                               int n_devices) {
+  if (n == 0) return SHF_HB_OK;
+  if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  const uint8_t* k = (const uint8_t*)keys;
+  return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
+    return host_fixed(k ? k + lo * key_len : nullptr, key_len, hi - lo, seed, out + lo);
+  });
+}
+
+int shf_hash_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed,
+                             shf_hash128* out, int n_devices) {
+  if (n == 0) return SHF_HB_OK;
+  if (!out || !offsets || !bytes) return SHF_HB_ERR_ARG;
+  int rc = check_var_lengths_host(offsets, n);
+  if (rc) return rc;
+  const uint8_t* b = (const uint8_t*)bytes;
+  return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
+    return host_var(b, offsets + lo, hi - lo, seed, out + lo);
+  });
+}
+
+int shf_hash_batch_device_count(void) { return visible_devices(); }
+
+int shf_hash_batch_check_device(void) {
+  DevCtx* c = nullptr;
+  return current_ctx(&c);
+}
+
+int shf_hash_batch_last_hip_error(void) { return tls_last_hip; }
+
+const char* shf_hash_batch_strerror(int status) {
+  switch (status) {
+    case SHF_HB_OK:
+      return "ok";
+    case SHF_HB_ERR_ARG:
+      return "invalid argument";
+    case SHF_HB_ERR_NODEV:
+      return "no HIP device available";
+    case SHF_HB_ERR_HIP:
+      return "HIP runtime error";
+    case SHF_HB_ERR_NOMEM:
+      return "out of device or pinned host memory";
+    case SHF_HB_ERR_ARCH:
+      return "device is not gfx950 (MI355X)";
+    default:
+      return "unknown status";
+  }
+}
+
+const char* shf_hash_batch_version(void) { return "shf_hash_batch 0.1 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+"""The C-ABI library: loads, exports every declared symbol, validates arguments
+and fails loudly (never silently on the CPU) when no GPU is present.
+
+No hashing is executed here; parity lives in tests/test_gpu_parity.py (-m gpu).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import sharedhashfile_amd as hbmod
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def test_library_exports_every_header_symbol(hb):
+    declared = hbmod.header_functions()
+    assert len(declared) >= 14
+    out = subprocess.check_output(["nm", "-D", "--defined-only", hbmod.LIB_PATH]).decode()
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    # nothing else leaks out of the shared object (hidden visibility)
+    extra = sorted(s for s in exported if not s.startswith("shf_"))
+    assert not extra, extra
+
+
+def test_header_compiles_as_c():
+    src = '#include "shf_hash_batch.h"\nint main(void){ shf_hash128 h; (void)h; return SHF_HB_OK; }\n'
+    p = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-x", "c", "-",
+                        "-o", "/dev/null"], input=src.encode(), capture_output=True)
+    assert p.returncode == 0, p.stderr.decode()
+
+
+def test_record_layout_matches_shf_hash():
+    # SHF_HASH: 16-byte packed union, u64[0]=h1, u64[1]=h2 (shf.private.h:180-185).
+    src = ('#include <stddef.h>\n#include "shf_hash_batch.h"\n'
+           '_Static_assert(sizeof(shf_hash128) == 16, "size");\n'
+           '_Static_assert(offsetof(shf_hash128, h2) == 8, "h2");\nint main(void){return 0;}\n')
+    p = subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-x", "c", "-", "-o", "/dev/null"],
+                       input=src.encode(), capture_output=True)
+    assert p.returncode == 0, p.stderr.decode()
+
+
+def test_strerror_and_version(hb):
+    lib = hb.load()
+    names = {s: lib.shf_hash_batch_strerror(s).decode() for s in (0, -1, -2, -3, -4, -5, -99)}
+    assert names[0] == "ok" and names[-99] == "unknown status"
+    assert len(set(names.values())) == 7
+    assert b"gfx950" in lib.shf_hash_batch_version()
+
+
+def test_argument_validation_needs_no_device(hb):
+    lib = hb.load()
+    keys = np.zeros(64, dtype=np.uint8)
+    out = np.zeros((4, 2), dtype=np.uint64)
+    # n == 0 is a no-op success, whatever the pointers
+    assert lib.shf_hash_batch_fixed(None, 16, 0, 12345, None, hbmod.MEM_HOST) == hbmod.OK
+    assert lib.shf_hash_batch_var(None, None, 0, 12345, None, hbmod.MEM_DEVICE) == hbmod.OK
+    # NULL output / NULL keys with key_len > 0
+    assert lib.shf_hash_batch_fixed(keys.ctypes.data, 16, 4, 12345, None, hbmod.MEM_HOST) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_fixed(None, 16, 4, 12345, out.ctypes.data, hbmod.MEM_HOST) == hbmod.ERR_ARG
+    # key_len >= 2^31 (reference takes `const int len`, murmurhash3.c:75)
+    assert lib.shf_hash_batch_fixed(keys.ctypes.data, 0x80000000, 4, 12345, out.ctypes.data,
+                                    hbmod.MEM_HOST) == hbmod.ERR_ARG
+    # unknown memory kind
+    assert lib.shf_hash_batch_fixed(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 7) == hbmod.ERR_ARG
+    # var: decreasing offsets / too-long key are rejected on the host path
+    off = np.array([0, 8, 4], dtype=np.uint64)
+    assert lib.shf_hash_batch_var(keys.ctypes.data, off.ctypes.data, 2, 12345, out.ctypes.data,
+                                  hbmod.MEM_HOST) == hbmod.ERR_ARG
+    off = np.array([0, 1 << 31], dtype=np.uint64)
+    assert lib.shf_hash_batch_var(keys.ctypes.data, off.ctypes.data, 1, 12345, out.ctypes.data,
+                                  hbmod.MEM_HOST) == hbmod.ERR_ARG
+    # forced kernels with shapes they cannot take
+    assert lib.shf_hash_batch_fixed_kernel_async(keys.ctypes.data, 17, 3, 12345, out.ctypes.data,
+                                                 hbmod.KERNEL_FIXED16, None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_fixed_kernel_async(keys.ctypes.data, 24, 2, 12345, out.ctypes.data,
+                                                 hbmod.KERNEL_TILED, None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_fixed_kernel_async(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 9,
+                                                 None) == hbmod.ERR_ARG
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device behaviour")
+def test_no_device_fails_loudly_not_on_cpu(hb):
+    lib = hb.load()
+    keys = np.zeros(64, dtype=np.uint8)
+    out = np.zeros((4, 2), dtype=np.uint64)
+    rc = lib.shf_hash_batch_fixed(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, hbmod.MEM_HOST)
+    assert rc in (hbmod.ERR_NODEV, hbmod.ERR_HIP)
+    assert not out.any()  # nothing computed on the CPU behind our back
+    assert lib.shf_hash_batch_check_device() in (hbmod.ERR_NODEV, hbmod.ERR_HIP)
+    with pytest.raises(hbmod.ShfHashBatchError):
+        hbmod.hash_fixed_host(keys.reshape(4, 16))
+    assert lib.shf_hash_batch_fixed_multi(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 0) in (
+        hbmod.ERR_NODEV, hbmod.ERR_HIP)
+
+
+def test_missing_library_raises(tmp_path):
+    with pytest.raises(RuntimeError):
+        hbmod.load(str(tmp_path / "nope.so"))

@@ -1,0 +1,272 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the reference goldens.
+
+Bar: bit-exact, all 128 bits of every SHF_HASH (and every packed UID-parts word).
+Runs only on a real MI355X: python -m pytest tests -m gpu
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from sharedhashfile_amd.keygen import counter_keys, splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev(hb):
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    hb.check_device()  # raises unless the current device is gfx950
+    return torch.device("cuda:0")
+
+
+def u64(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64)
+
+
+def d_u8(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8).reshape(-1)).to(dev)
+
+
+def d_off(off, dev):
+    return torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(dev)
+
+
+def fixed_kernels(key_len, aligned=True):
+    ks = [0, 3]  # AUTO, GENERIC
+    if key_len == 16 and aligned:
+        ks.append(1)
+    if key_len >= 32 and key_len % 16 == 0 and aligned:
+        ks.append(2)
+    return ks
+
+
+# ---------------------------------------------------------------------------
+# reference goldens
+# ---------------------------------------------------------------------------
+def test_golden_cases(hb, dev, golden):
+    for c in golden["cases"]:
+        key = bytes.fromhex(c["key_hex"])
+        want = np.array([int(c["h1"], 16), int(c["h2"], 16)], dtype=np.uint64)
+        L = len(key)
+        keys = d_u8(np.frombuffer(key, dtype=np.uint8) if L else np.zeros(16, np.uint8), dev)
+        for k in fixed_kernels(L):
+            got = u64(hb.hash_fixed(keys, L, seed=c["seed"], kernel=k) if L else
+                      hb.hash_fixed(keys[:0], 0, seed=c["seed"], kernel=k))
+            if L == 0:
+                assert got.shape[0] == 0
+                continue
+            assert np.array_equal(got[0], want), (c["name"], k)
+        # the same key through the variable-length path
+        off = d_off(np.array([0, L], dtype=np.uint64), dev)
+        got = u64(hb.hash_var(keys, off, seed=c["seed"]))
+        assert np.array_equal(got[0], want), c["name"]
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3, 5, 8, 15])
+def test_var_golden_any_alignment(hb, dev, golden_var, shift):
+    data = np.concatenate([np.full(shift, 0xA5, np.uint8), golden_var["bytes"], np.full(3, 0x5A, np.uint8)])
+    off = golden_var["offsets"] + np.uint64(shift)
+    got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev)))
+    assert np.array_equal(got, golden_var["hashes"])
+
+
+@pytest.mark.parametrize("width", [4, 16])
+def test_counter_keys_test9_shape(hb, dev, golden, width):
+    g = golden["counters"]["counter_w%d" % width]
+    keys = d_u8(counter_keys(g["count"], width), dev)
+    for k in fixed_kernels(width):
+        got = u64(hb.hash_fixed(keys, width, kernel=k))
+        assert hashlib.sha256(got.astype("<u8").tobytes()).hexdigest() == g["sha256_of_hashes"], k
+
+
+@pytest.mark.parametrize("name", ["fixed_w16", "fixed_w256"])
+def test_fixed_random_golden(hb, dev, golden, name):
+    g = golden["fixed"][name]
+    flat = np.frombuffer(splitmix_bytes(g["key_len"] * g["count"], int(g["splitmix_stream"], 16)), dtype=np.uint8)
+    keys = d_u8(flat, dev)
+    for k in fixed_kernels(g["key_len"]):
+        got = u64(hb.hash_fixed(keys, g["key_len"], kernel=k))
+        assert hashlib.sha256(got.astype("<u8").tobytes()).hexdigest() == g["sha256_of_hashes"], k
+
+
+# ---------------------------------------------------------------------------
+# oracle parity over shapes and edge cases
+# ---------------------------------------------------------------------------
+LENGTHS = list(range(0, 81)) + [95, 96, 97, 112, 127, 128, 129, 144, 160, 240, 255, 256, 257, 272, 384, 511, 512,
+                                528, 1024, 1040, 4096]
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000])
+def test_fixed_all_lengths_all_kernels(hb, dev, oracle, n):
+    rng = np.random.default_rng(n)
+    for L in LENGTHS:
+        if L == 0:
+            continue
+        flat = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+        want = oracle.hash_fixed(flat, L)
+        keys = d_u8(flat, dev)
+        for k in fixed_kernels(L):
+            got = u64(hb.hash_fixed(keys, L, kernel=k))
+            assert np.array_equal(got, want), (L, n, k)
+
+
+def test_zero_length_keys(hb, dev, oracle):
+    want = oracle.hash(b"")
+    keys = torch.zeros(16, dtype=torch.uint8, device=dev)
+    out = torch.zeros((5, 2), dtype=torch.int64, device=dev)
+    rc = hb.load().shf_hash_batch_fixed_async(keys.data_ptr(), 0, 5, 12345, out.data_ptr(), None)
+    assert rc == 0
+    got = u64(out)
+    assert all(tuple(int(x) for x in r) == want for r in got)
+    off = d_off(np.zeros(6, dtype=np.uint64), dev)
+    got = u64(hb.hash_var(keys, off))
+    assert all(tuple(int(x) for x in r) == want for r in got)
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3, 4, 7, 13])
+def test_fixed_unaligned_buffer(hb, dev, oracle, shift):
+    rng = np.random.default_rng(shift)
+    for L in [16, 32, 100, 256]:
+        n = 777
+        flat = rng.integers(0, 256, size=n * L + shift, dtype=np.uint8)
+        want = oracle.hash_fixed(flat[shift:], L)
+        keys = d_u8(flat, dev)[shift:]
+        got = u64(hb.hash_fixed(keys, L))  # AUTO must notice the misalignment
+        assert np.array_equal(got, want), (L, shift)
+
+
+def test_var_random_lengths(hb, dev, oracle):
+    rng = np.random.default_rng(7)
+    for lo, hi, n in [(0, 16, 5000), (8, 512, 20000), (0, 2000, 3000), (500, 5000, 300)]:
+        lens = rng.integers(lo, hi + 1, size=n)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        data = rng.integers(0, 256, size=int(off[-1]) + 1, dtype=np.uint8)
+        got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev)))
+        assert np.array_equal(got, oracle.hash_var(data, off)), (lo, hi)
+
+
+def test_var_long_keys(hb, dev, oracle):
+    lens = np.array([65537, 1 << 20, 3, (1 << 20) + 15, 0, 100000], dtype=np.uint64)
+    off = np.zeros(lens.size + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]), 99), dtype=np.uint8)
+    got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev)))
+    assert np.array_equal(got, oracle.hash_var(data, off))
+
+
+def test_var_offsets_beyond_4gib(hb, dev, oracle):
+    """64-bit offsets: keys living past the first 4 GiB of the byte buffer."""
+    base = (1 << 32) + 12345
+    n = 2000
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 300, size=n)
+    rel = np.zeros(n + 1, dtype=np.uint64)
+    rel[1:] = np.cumsum(lens)
+    payload = rng.integers(0, 256, size=int(rel[-1]), dtype=np.uint8)
+    big = torch.empty(base + int(rel[-1]) + 64, dtype=torch.uint8, device=dev)
+    big[base:base + payload.size] = torch.from_numpy(payload).to(dev)
+    got = u64(hb.hash_var(big, d_off(rel + np.uint64(base), dev)))
+    assert np.array_equal(got, oracle.hash_var(payload, rel))
+    del big
+    torch.cuda.empty_cache()
+
+
+def test_seeds(hb, dev, oracle):
+    rng = np.random.default_rng(11)
+    flat = rng.integers(0, 256, size=300 * 48, dtype=np.uint8)
+    keys = d_u8(flat, dev)
+    for seed in [0, 1, 12345, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF]:
+        for k in fixed_kernels(48):
+            got = u64(hb.hash_fixed(keys, 48, seed=seed, kernel=k))
+            assert np.array_equal(got, oracle.hash_fixed(flat, 48, seed=seed)), (seed, k)
+
+
+def test_uid_parts(hb, dev, oracle, golden_var):
+    rng = np.random.default_rng(5)
+    for L in [4, 16, 256, 37]:
+        flat = rng.integers(0, 256, size=3000 * L, dtype=np.uint8)
+        want = oracle.uid_parts(oracle.hash_fixed(flat, L))
+        got = u64(hb.uid_parts_fixed(d_u8(flat, dev), L))
+        assert np.array_equal(got, want), L
+    got = u64(hb.uid_parts_var(d_u8(golden_var["bytes"], dev), d_off(golden_var["offsets"], dev)))
+    assert np.array_equal(got, oracle.uid_parts(golden_var["hashes"]))
+
+
+def test_async_on_side_stream(hb, dev, oracle):
+    rng = np.random.default_rng(8)
+    flat = rng.integers(0, 256, size=100000 * 16, dtype=np.uint8)
+    keys = d_u8(flat, dev)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        out = hb.hash_fixed(keys, 16, stream=s)
+    s.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), oracle.hash_fixed(flat, 16))
+
+
+# ---------------------------------------------------------------------------
+# host-memory and multi-device entry points
+# ---------------------------------------------------------------------------
+def test_host_fixed_multi_chunk(hb, dev, oracle):
+    n = 5_000_000  # 80 MB of 16-B keys: more than one 64 MiB staging chunk
+    flat = np.frombuffer(splitmix_bytes(n * 16, 21), dtype=np.uint8)
+    got = hb.hash_fixed_host(flat, 16)
+    assert np.array_equal(got, oracle.hash_fixed(flat, 16, threads=8))
+    got = hb.hash_fixed_host(flat, 16, n_devices=0)
+    assert np.array_equal(got, oracle.hash_fixed(flat, 16, threads=8))
+
+
+def test_host_var_multi_chunk(hb, dev, oracle):
+    rng = np.random.default_rng(12)
+    n = 300_000
+    lens = rng.integers(8, 513, size=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)  # ~78 MB of key bytes
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    want = oracle.hash_var(data, off)
+    assert np.array_equal(hb.hash_var_host(data, off), want)
+    assert np.array_equal(hb.hash_var_host(data, off, n_devices=0), want)
+
+
+def test_host_huge_single_key(hb, dev, oracle):
+    n_big = (70 << 20) + 9  # one key larger than a staging chunk
+    data = np.frombuffer(splitmix_bytes(n_big + 100, 5), dtype=np.uint8)
+    off = np.array([0, 50, 50 + n_big, n_big + 100], dtype=np.uint64)
+    assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
+
+
+# ---------------------------------------------------------------------------
+# full-size properties (bench shapes): kernels agree, sampled oracle parity
+# ---------------------------------------------------------------------------
+def _sample_check(oracle, keys_dev, L, got, count=20000, seed=0):
+    n = got.shape[0]
+    idx = np.unique(np.random.default_rng(seed).integers(0, n, size=count))
+    rows = keys_dev.view(-1, L)[torch.from_numpy(idx).to(keys_dev.device)].cpu().numpy()
+    assert np.array_equal(got[idx], oracle.hash_fixed(rows, L))
+
+
+def test_config_b_10m_16b(hb, dev, oracle):
+    n, L = 10_000_000, 16
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+    a = hb.hash_fixed(keys, L, kernel=1)
+    b = hb.hash_fixed(keys, L, kernel=3)
+    assert torch.equal(a, b)
+    _sample_check(oracle, keys, L, u64(a))
+    # uid parts are a function of the hash (shf.c:800-803)
+    p = hb.uid_parts_fixed(keys, L)
+    h1, h2 = a[:, 0], a[:, 1]
+    want = (h1 & 0xFF) | (((h1 >> 16) & 0x7FF) << 8) | (((h1 >> 32) & 0x1FF) << 19) | ((h2 & 0x1FFFFF) << 32)
+    assert torch.equal(p, want)
+
+
+def test_256b_kernels_agree(hb, dev, oracle):
+    n, L = 2_000_003, 256
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+    a = hb.hash_fixed(keys, L, kernel=2)
+    b = hb.hash_fixed(keys, L, kernel=3)
+    assert torch.equal(a, b)
+    _sample_check(oracle, keys, L, u64(a))
