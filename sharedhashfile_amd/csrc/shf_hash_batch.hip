@@ -222,7 +222,13 @@ int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t
     }
     const uint64_t cnt = i1 - i0;
     const size_t nb = (size_t)(offsets[i1] - base);
-    if ((rc = ensure_staging(c, std::max(nb, (size_t)1), (size_t)std::max<uint64_t>(cnt, max_keys)))) return rc;
+    const size_t need_keys = (size_t)std::max<uint64_t>(cnt, max_keys);
+    if (nb > c->in_cap || need_keys > c->key_cap) {
+      // growing the staging buffers frees them: collect every chunk in flight first
+      for (int s = 0; s < kSlots; ++s)
+        if ((rc = drain_slot(c, s, pend[s]))) return rc;
+      if ((rc = ensure_staging(c, std::max(nb, (size_t)1), need_keys))) return rc;
+    }
     const int s = (int)(idx % kSlots);
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
     if (nb) memcpy(c->h_in[s], bytes + base, nb);
