@@ -33,6 +33,7 @@ KERNEL_AUTO = 0
 KERNEL_FIXED16 = 1
 KERNEL_TILED = 2
 KERNEL_GENERIC = 3
+KERNEL_SPAN = 4
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libshf_hash_batch.so")
@@ -73,6 +74,7 @@ _SIGS = {
     "shf_hash_batch_fixed_multi": [_VP, _U32, _U64, _U32, _VP, _INT],
     "shf_hash_batch_var_multi": [_VP, _VP, _U64, _U32, _VP, _INT],
     "shf_hash_batch_fixed_kernel_async": [_VP, _U32, _U64, _U32, _VP, _INT, _VP],
+    "shf_hash_batch_var_kernel_async": [_VP, _VP, _U64, _U32, _VP, _INT, _VP],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
@@ -156,7 +158,7 @@ def hash_fixed(keys, key_len=None, seed=SEED, out=None, stream=None, kernel=KERN
     return out
 
 
-def hash_var(data, offsets, seed=SEED, out=None, stream=None):
+def hash_var(data, offsets, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO):
     """Hash n variable-length keys on the GPU: key i = data[offsets[i]:offsets[i+1]].
 
     data: uint8 CUDA tensor; offsets: int64 CUDA tensor of n + 1 entries.
@@ -167,10 +169,10 @@ def hash_var(data, offsets, seed=SEED, out=None, stream=None):
     n = offsets.numel() - 1
     if out is None:
         out = torch.empty((max(n, 0), 2), dtype=torch.int64, device=data.device)
-    rc = load().shf_hash_batch_var_async(
+    rc = load().shf_hash_batch_var_kernel_async(
         ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
-        ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
-    _check(rc, "shf_hash_batch_var_async")
+        ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
+    _check(rc, "shf_hash_batch_var_kernel_async")
     return out
 
 

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "murmur3_mix.h"
 #include "kernels.h"
 
@@ -146,6 +148,9 @@ __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ byt
 // (8 lanes per row) cover a row's 32 banks once; the lane-per-key reads of one
 // piece index hit 16 distinct (k&1, slot) pairs per ds_read_b128 lane group, so
 // both sides are conflict free.
+// The grid is sized to exactly the resident workgroups (launch_fixed), every
+// wave walks tiles with a grid stride and prefetches round r+1 into registers
+// while hashing round r out of LDS.
 // ---------------------------------------------------------------------------
 constexpr int kTileKeys = 64;
 constexpr int kRoundBlocks = 8;
@@ -177,14 +182,19 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
   auto fetch = [&](uint64_t tt, uint32_t r, u32x4 (&reg)[kRoundBlocks]) {
     const uint64_t k0 = tt * kTileKeys;
     const uint32_t rb = min((uint32_t)kRoundBlocks, nblocks - r * kRoundBlocks);
+    const bool full = rb == kRoundBlocks && k0 + kTileKeys <= n;
+    const uint8_t* src0 = keys + (k0 + ld_key_sub) * key_len + (uint64_t)r * 128u + 16u * ld_piece;
+    if (full) {  // common case: no per-lane predicate
 #pragma unroll
-    for (int q = 0; q < kRoundBlocks; ++q) {
-      const uint64_t key = k0 + 8u * q + ld_key_sub;
-      if (key < n && ld_piece < rb) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(keys + key * key_len + (uint64_t)r * 128u + 16u * ld_piece);
-        reg[q] = __builtin_nontemporal_load(src);
-      } else {
-        reg[q] = u32x4{0u, 0u, 0u, 0u};
+      for (int q = 0; q < kRoundBlocks; ++q)
+        reg[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src0 + (uint64_t)(8u * q) * key_len));
+    } else {
+#pragma unroll
+      for (int q = 0; q < kRoundBlocks; ++q) {
+        const uint64_t key = k0 + 8u * q + ld_key_sub;
+        reg[q] = (key < n && ld_piece < rb)
+                     ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src0 + (uint64_t)(8u * q) * key_len))
+                     : u32x4{0u, 0u, 0u, 0u};
       }
     }
   };
@@ -202,8 +212,18 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // Prefetch the next round (or the next tile's first round).
     const uint32_t rb = min((uint32_t)kRoundBlocks, nblocks - r * kRoundBlocks);
+    // Read this round's blocks of this lane's key (all reads in flight at once).
+    u32x4 b[kRoundBlocks];
+#pragma unroll
+    for (int j = 0; j < kRoundBlocks; ++j)
+      b[j] = ((uint32_t)j < rb) ? *reinterpret_cast<const u32x4*>(tile + tile_slot(lane, (uint32_t)j))
+                                : u32x4{0u, 0u, 0u, 0u};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // Prefetch the next round (or the next tile's first round).
     uint64_t t_next = t;
     uint32_t r_next = r + 1;
     if (r_next == rounds) {
@@ -213,17 +233,9 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
     const bool more = t_next < ntiles;
     if (more) fetch(t_next, r_next, nxt);
 
-    // Hash this round's blocks of this lane's key.
 #pragma unroll
-    for (int j = 0; j < kRoundBlocks; ++j) {
-      if ((uint32_t)j < rb) {
-        const u32x4 b = *reinterpret_cast<const u32x4*>(tile + tile_slot(lane, (uint32_t)j));
-        body_block(s, pack64(b.x, b.y), pack64(b.z, b.w));
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = 0; j < kRoundBlocks; ++j)
+      if ((uint32_t)j < rb) body_block(s, pack64(b[j].x, b[j].y), pack64(b[j].z, b[j].w));
 
     if (r + 1 == rounds) {
       const uint64_t key = t * kTileKeys + lane;
@@ -238,8 +250,189 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
 }
 
 // ---------------------------------------------------------------------------
+// Span kernel: variable-length keys (offset array) and fixed lengths the tiled
+// kernel cannot take. One wave (= one workgroup) owns a tile of 64 consecutive
+// keys, whose bytes are one contiguous span of the packed buffer. The span is
+// fetched with fully coalesced 16-B loads (1 KiB per wave instruction) into
+// registers one tile ahead, staged in LDS, and each lane then hashes its own
+// key out of LDS with dword reads funnel-shifted by v_alignbyte_b32 (keys start
+// at any byte). A tile whose span exceeds the LDS window is hashed straight
+// from global memory (wave-uniform fallback; rare for keys <= 320 B).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSpanCap = 20u * 1024u;      // LDS bytes per wave
+constexpr int kSpanPieces = kSpanCap / 1024u;   // 16-B pieces per lane per full span
+
+template <bool VAR>
+struct SpanTile {
+  uint64_t key;       // this lane's key index
+  uint64_t start;     // byte offset of this lane's key (relative to `bytes`)
+  uint32_t len;       // this lane's key length
+  bool valid;         // key < n
+  uint64_t base;      // absolute address of the span's first 16-B piece (uniform)
+  uint32_t span16;    // bytes to stage, multiple of 16 (uniform; > kSpanCap -> fallback)
+};
+
+template <bool VAR>
+__device__ __forceinline__ SpanTile<VAR> span_tile(const uint8_t* bytes, const uint64_t* offsets, uint64_t off_base,
+                                                   uint32_t key_len, uint64_t n, uint64_t t, uint32_t lane) {
+  SpanTile<VAR> ti;
+  const uint64_t k0 = t * 64u;
+  const uint32_t kn = (uint32_t)min<uint64_t>(64u, n - k0);
+  ti.key = k0 + lane;
+  ti.valid = lane < kn;
+  uint64_t first, end;  // tile bytes [first, end) relative to `bytes` (wave-uniform)
+  if constexpr (VAR) {
+    const uint64_t o0 = ti.valid ? offsets[ti.key] : 0, o1 = ti.valid ? offsets[ti.key + 1] : 0;
+    ti.start = o0 - off_base;
+    ti.len = (uint32_t)(o1 - o0);
+    const uint64_t e_rel = o1 - off_base;
+    first = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ti.start) |
+            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ti.start >> 32)) << 32);
+    end = (uint64_t)__builtin_amdgcn_readlane((uint32_t)e_rel, kn - 1) |
+          ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(e_rel >> 32), kn - 1) << 32);
+  } else {
+    ti.start = ti.key * (uint64_t)key_len;
+    ti.len = key_len;
+    first = k0 * (uint64_t)key_len;
+    end = (k0 + kn) * (uint64_t)key_len;
+  }
+  if (end <= first) {  // every key of the tile is empty: stage and load nothing
+    ti.base = 0;
+    ti.span16 = 0;
+    return ti;
+  }
+  const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
+  ti.base = (b + first) & ~(uint64_t)15;
+  const uint64_t span = ((b + end + 15) & ~(uint64_t)15) - ti.base;
+  ti.span16 = span > 0xffffffffull ? 0xffffffffu : (uint32_t)span;
+  return ti;
+}
+
+// Fetch the span into registers: piece q of lane l covers bytes q*1024 + 16l.
+// Only 16-B pieces holding at least one byte of the tile are loaded, so no load
+// can touch a page the keys do not.
+__device__ __forceinline__ void span_fetch(u32x4 (&reg)[kSpanPieces], uint64_t base, uint32_t span16, uint32_t lane) {
+  const u32x4* src = reinterpret_cast<const u32x4*>(base) + lane;
+#pragma unroll
+  for (int q = 0; q < kSpanPieces; ++q) {
+    const uint32_t off = (uint32_t)q * 1024u + lane * 16u;
+    if ((uint32_t)q * 1024u < span16) reg[q] = off < span16 ? __builtin_nontemporal_load(src + 64 * q) : u32x4{0, 0, 0, 0};
+  }
+}
+
+__device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[kSpanPieces], uint32_t span16,
+                                           uint32_t lane) {
+#pragma unroll
+  for (int q = 0; q < kSpanPieces; ++q)
+    if ((uint32_t)q * 1024u < span16) reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
+}
+
+// Hash `len` bytes starting at byte offset p of the staged span. Only dwords
+// holding bytes of the key are read (plus none past the staged region).
+__device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
+  const uint32_t sh = p & 3u;
+  const uint32_t* w = lds + (p >> 2);
+  const uint32_t nblocks = len >> 4;
+  State s{seed, seed};
+  uint32_t x0 = (len > 0) ? w[0] : 0u;
+  for (uint32_t j = 0; j < nblocks; ++j) {
+    const uint32_t* v = w + 4 * j;
+    const uint32_t x1 = v[1], x2 = v[2], x3 = v[3];
+    const bool need4 = sh != 0 || j + 1 < nblocks || (len & 15u) != 0;
+    const uint32_t x4 = need4 ? v[4] : 0u;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+    body_block(s, pack64(d0, d1), pack64(d2, d3));
+    x0 = x4;
+  }
+  const uint32_t rem = len & 15u;
+  if (rem) {
+    const uint32_t* t = w + 4 * nblocks;
+    const uint32_t need = sh + rem;
+    uint32_t x[5];
+    x[0] = x0;
+#pragma unroll
+    for (int q = 1; q < 5; ++q) x[q] = (4u * q < need) ? t[q] : 0u;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
+    const uint64_t t1 = pack64(d0, d1) & low_bytes_mask(rem);
+    const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
+    tail_block(s, t1, t2, rem);
+  }
+  finish(s, len);
+  return s;
+}
+
+template <int OUT, bool VAR>
+__global__ __launch_bounds__(64) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
+                                             uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
+                                             void* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t ntiles = (n + 63) / 64;
+  const uint64_t stride = gridDim.x;
+  uint64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+
+  u32x4 reg[kSpanPieces];
+  SpanTile<VAR> cur = span_tile<VAR>(bytes, offsets, off_base, key_len, n, t, lane);
+  if (cur.span16 <= kSpanCap) span_fetch(reg, cur.base, cur.span16, lane);
+  uint64_t t_next = t + stride;
+  SpanTile<VAR> nxt{};
+  if (t_next < ntiles) nxt = span_tile<VAR>(bytes, offsets, off_base, key_len, n, t_next, lane);
+
+  while (true) {
+    const bool staged = cur.span16 <= kSpanCap;
+    if (staged) span_stage(span_lds, reg, cur.span16, lane);
+    __syncthreads();
+    // prefetch the next tile's span while this one is hashed
+    const bool more = t_next < ntiles;
+    if (more && nxt.span16 <= kSpanCap) span_fetch(reg, nxt.base, nxt.span16, lane);
+    const uint64_t t_nn = t_next + stride;
+    SpanTile<VAR> nn{};
+    if (t_nn < ntiles) nn = span_tile<VAR>(bytes, offsets, off_base, key_len, n, t_nn, lane);
+
+    if (cur.valid) {
+      State s;
+      if (staged) {
+        const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + cur.start - cur.base);
+        s = hash_lds(span_lds, p, cur.len, seed);
+      } else {
+        s = hash_bytes(bytes + cur.start, cur.len, seed);
+      }
+      store_result<OUT>(out, cur.key, s);
+    }
+    __syncthreads();
+    if (!more) break;
+    cur = nxt;
+    nxt = nn;
+    t_next = t_nn;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+// Workgroups of `kernel` that fit on the whole device at once (cached per device).
+static unsigned resident_grid(const void* kernel, int block, size_t dyn_lds, int slot) {
+  static std::atomic<unsigned> cache[16][8];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  unsigned g = cache[dev][slot].load(std::memory_order_relaxed);
+  if (g) return g;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  g = (unsigned)(per_cu * cus);
+  cache[dev][slot].store(g, std::memory_order_relaxed);
+  return g;
+}
+
 static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
   uint64_t g = (items + per_block - 1) / per_block;
   if (g > cap) g = cap;
@@ -247,29 +440,44 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
   return (unsigned)g;
 }
 
+template <int OUT, bool VAR>
+static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
+                              uint64_t n, uint32_t seed, void* out, hipStream_t st) {
+  const uint64_t tiles = (n + 63) / 64;
+  const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR>), 64, kSpanCap,
+                                     2 + OUT * 2 + (VAR ? 1 : 0));
+  hipLaunchKernelGGL((k_span<OUT, VAR>), dim3(grid_for(tiles, 1, res)), dim3(64), kSpanCap, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, out);
+  return hipGetLastError();
+}
+
 template <int OUT>
 static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out,
                                  hipStream_t st, int kernel) {
-  const unsigned cap = 256u * 32u;  // 256 CUs x 8 blocks x 4 waves of grid-stride
+  const unsigned cap = 256u * 32u;
+  const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
   if (kernel == kKernelAuto) {
-    if (key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0) kernel = kKernelFixed16;
-    else if (key_len >= 32 && (key_len & 15u) == 0 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0)
-      kernel = kKernelTiled;
+    if (key_len == 16 && al16) kernel = kKernelFixed16;
+    else if (key_len >= 32 && (key_len & 15u) == 0 && al16) kernel = kKernelTiled;
+    else if ((uint64_t)key_len * 64u + 16u <= kSpanCap) kernel = kKernelSpan;
     else kernel = kKernelGeneric;
   }
   switch (kernel) {
     case kKernelFixed16:
-      if (key_len != 16 || (reinterpret_cast<uintptr_t>(keys) & 15u)) return hipErrorInvalidValue;
+      if (key_len != 16 || !al16) return hipErrorInvalidValue;
       hipLaunchKernelGGL(k_fixed16<OUT>, dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
                          reinterpret_cast<const u32x4*>(keys), n, seed, out);
       break;
     case kKernelTiled: {
-      if (key_len < 16 || (key_len & 15u) || (reinterpret_cast<uintptr_t>(keys) & 15u)) return hipErrorInvalidValue;
+      if (key_len < 32 || (key_len & 15u) || !al16) return hipErrorInvalidValue;
       const uint64_t tiles = (n + kTileKeys - 1) / kTileKeys;
-      hipLaunchKernelGGL(k_tiled<OUT>, dim3(grid_for(tiles, kTiledWaves, 256u * 8u)), dim3(64 * kTiledWaves), 0, st,
+      const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_tiled<OUT>), 64 * kTiledWaves, 0, OUT);
+      hipLaunchKernelGGL(k_tiled<OUT>, dim3(grid_for(tiles, kTiledWaves, res)), dim3(64 * kTiledWaves), 0, st,
                          reinterpret_cast<const uint8_t*>(keys), key_len, n, seed, out);
       break;
     }
+    case kKernelSpan:
+      return launch_span<OUT, false>(keys, nullptr, 0, key_len, n, seed, out, st);
     default:
       hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
                          reinterpret_cast<const uint8_t*>(keys), (const uint64_t*)nullptr, (uint64_t)0, key_len, n,
@@ -281,11 +489,14 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
 
 template <int OUT>
 static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                               uint32_t seed, void* out, hipStream_t st) {
-  const unsigned cap = 256u * 32u;
-  hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, out);
-  return hipGetLastError();
+                               uint32_t seed, void* out, hipStream_t st, int kernel) {
+  if (kernel == kKernelGeneric) {
+    const unsigned cap = 256u * 32u;
+    hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, out);
+    return hipGetLastError();
+  }
+  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, out, st);
 }
 
 hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out, int out_mode,
@@ -296,10 +507,10 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
 }
 
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
-                      void* out, int out_mode, hipStream_t st) {
+                      void* out, int out_mode, hipStream_t st, int kernel) {
   if (n == 0) return hipSuccess;
-  return out_mode == kOutHash ? launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, out, st)
-                              : launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, out, st);
+  return out_mode == kOutHash ? launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, out, st, kernel)
+                              : launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, out, st, kernel);
 }
 
 }  // namespace shfhb

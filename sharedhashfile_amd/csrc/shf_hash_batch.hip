@@ -265,12 +265,12 @@ int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, 
 }
 
 int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, void* out, int out_mode,
-               hipStream_t st, bool sync) {
+               hipStream_t st, bool sync, int kernel = shfhb::kKernelAuto) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
   if (sync) st = c->st[0];
-  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, out, out_mode, st));
+  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, out, out_mode, st, kernel));
   if (sync) HB_TRY(hipStreamSynchronize(st));
   return SHF_HB_OK;
 }
@@ -344,7 +344,8 @@ int shf_hash_batch_fixed_kernel_async(const void* d_keys, uint32_t key_len, uint
                                       shf_hash128* d_out, int kernel, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
-  if (kernel < SHF_HB_KERNEL_AUTO || kernel > SHF_HB_KERNEL_GENERIC) return SHF_HB_ERR_ARG;
+  if (kernel < SHF_HB_KERNEL_AUTO || kernel > SHF_HB_KERNEL_SPAN) return SHF_HB_ERR_ARG;
+  if (kernel == SHF_HB_KERNEL_SPAN && (uint64_t)key_len * 64u + 16u > 20u * 1024u) return SHF_HB_ERR_ARG;
   if (kernel == SHF_HB_KERNEL_FIXED16 && (key_len != 16 || ((uintptr_t)d_keys & 15u))) return SHF_HB_ERR_ARG;
   if (kernel == SHF_HB_KERNEL_TILED && (key_len < 32 || (key_len & 15u) || ((uintptr_t)d_keys & 15u)))
     return SHF_HB_ERR_ARG;
@@ -369,6 +370,15 @@ int shf_hash_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uin
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, false);
+}
+
+int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
+                                    shf_hash128* d_out, int kernel, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
+  if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC)
+    return SHF_HB_ERR_ARG;
+  return device_var(d_bytes, d_offsets, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
 }
 
 int shf_uid_parts_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,

@@ -41,7 +41,12 @@ def fixed_kernels(key_len, aligned=True):
         ks.append(1)
     if key_len >= 32 and key_len % 16 == 0 and aligned:
         ks.append(2)
+    if key_len * 64 + 16 <= 20 * 1024:
+        ks.append(4)  # SPAN
     return ks
+
+
+VAR_KERNELS = [0, 3, 4]  # AUTO (= SPAN), GENERIC, SPAN
 
 
 # ---------------------------------------------------------------------------
@@ -62,16 +67,18 @@ def test_golden_cases(hb, dev, golden):
             assert np.array_equal(got[0], want), (c["name"], k)
         # the same key through the variable-length path
         off = d_off(np.array([0, L], dtype=np.uint64), dev)
-        got = u64(hb.hash_var(keys, off, seed=c["seed"]))
-        assert np.array_equal(got[0], want), c["name"]
+        for k in VAR_KERNELS:
+            got = u64(hb.hash_var(keys, off, seed=c["seed"], kernel=k))
+            assert np.array_equal(got[0], want), (c["name"], k)
 
 
 @pytest.mark.parametrize("shift", [0, 1, 2, 3, 5, 8, 15])
 def test_var_golden_any_alignment(hb, dev, golden_var, shift):
     data = np.concatenate([np.full(shift, 0xA5, np.uint8), golden_var["bytes"], np.full(3, 0x5A, np.uint8)])
     off = golden_var["offsets"] + np.uint64(shift)
-    got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev)))
-    assert np.array_equal(got, golden_var["hashes"])
+    for k in VAR_KERNELS:
+        got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k))
+        assert np.array_equal(got, golden_var["hashes"]), k
 
 
 @pytest.mark.parametrize("width", [4, 16])
@@ -146,8 +153,37 @@ def test_var_random_lengths(hb, dev, oracle):
         off = np.zeros(n + 1, dtype=np.uint64)
         off[1:] = np.cumsum(lens)
         data = rng.integers(0, 256, size=int(off[-1]) + 1, dtype=np.uint8)
-        got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev)))
-        assert np.array_equal(got, oracle.hash_var(data, off)), (lo, hi)
+        want = oracle.hash_var(data, off)
+        for k in VAR_KERNELS:
+            got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k))
+            assert np.array_equal(got, want), (lo, hi, k)
+
+
+def test_var_span_edges(hb, dev, oracle):
+    """Tiles with no bytes, tiles exactly filling / overflowing the 20 KiB LDS
+    window (global fallback), a last partial tile, buffers ending on a page."""
+    rng = np.random.default_rng(17)
+    cases = [
+        np.zeros(200, dtype=np.int64),                                 # every tile empty
+        np.concatenate([np.zeros(64, np.int64), rng.integers(0, 40, 100)]),
+        np.full(64, 320, dtype=np.int64),                              # 20480 B: exactly the window (aligned)
+        np.full(64, 319, dtype=np.int64),
+        np.full(130, 321, dtype=np.int64),                             # > window: fallback tiles
+        np.concatenate([np.full(63, 1, np.int64), [20000], np.full(65, 7, np.int64)]),
+        rng.integers(300, 340, size=1000),                             # straddles the window size
+    ]
+    for lens in cases:
+        off = np.zeros(lens.size + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        data = rng.integers(0, 256, size=max(int(off[-1]), 1), dtype=np.uint8)
+        want = oracle.hash_var(data, off)
+        # place the bytes so the buffer ends exactly at the end of a 4 KiB-aligned allocation
+        pad = (-int(off[-1])) % 4096
+        big = torch.zeros(pad + max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
+        big[pad:pad + int(off[-1])] = torch.from_numpy(data[:int(off[-1])]).to(dev)
+        for k in VAR_KERNELS:
+            got = u64(hb.hash_var(big, d_off(off + np.uint64(pad), dev), kernel=k))
+            assert np.array_equal(got, want), (lens[:3], k)
 
 
 def test_var_long_keys(hb, dev, oracle):
@@ -155,8 +191,10 @@ def test_var_long_keys(hb, dev, oracle):
     off = np.zeros(lens.size + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens)
     data = np.frombuffer(splitmix_bytes(int(off[-1]), 99), dtype=np.uint8)
-    got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev)))
-    assert np.array_equal(got, oracle.hash_var(data, off))
+    want = oracle.hash_var(data, off)
+    for k in VAR_KERNELS:
+        got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k))
+        assert np.array_equal(got, want), k
 
 
 def test_var_offsets_beyond_4gib(hb, dev, oracle):
@@ -170,8 +208,10 @@ def test_var_offsets_beyond_4gib(hb, dev, oracle):
     payload = rng.integers(0, 256, size=int(rel[-1]), dtype=np.uint8)
     big = torch.empty(base + int(rel[-1]) + 64, dtype=torch.uint8, device=dev)
     big[base:base + payload.size] = torch.from_numpy(payload).to(dev)
-    got = u64(hb.hash_var(big, d_off(rel + np.uint64(base), dev)))
-    assert np.array_equal(got, oracle.hash_var(payload, rel))
+    want = oracle.hash_var(payload, rel)
+    for k in VAR_KERNELS:
+        got = u64(hb.hash_var(big, d_off(rel + np.uint64(base), dev), kernel=k))
+        assert np.array_equal(got, want), k
     del big
     torch.cuda.empty_cache()
 
