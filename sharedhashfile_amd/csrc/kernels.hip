@@ -286,10 +286,11 @@ __device__ __forceinline__ SpanTile<VAR> span_tile(const uint8_t* bytes, const u
     ti.start = o0 - off_base;
     ti.len = (uint32_t)(o1 - o0);
     const uint64_t e_rel = o1 - off_base;
-    first = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ti.start) |
-            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ti.start >> 32)) << 32);
-    end = (uint64_t)__builtin_amdgcn_readlane((uint32_t)e_rel, kn - 1) |
-          ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(e_rel >> 32), kn - 1) << 32);
+    // the readlane builtins return a signed int: widen through uint32_t, never sign-extend
+    first = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ti.start) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ti.start >> 32)) << 32);
+    end = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)e_rel, kn - 1) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(e_rel >> 32), kn - 1) << 32);
   } else {
     ti.start = ti.key * (uint64_t)key_len;
     ti.len = key_len;

@@ -186,6 +186,27 @@ def test_var_span_edges(hb, dev, oracle):
             assert np.array_equal(got, want), (lens[:3], k)
 
 
+def test_var_many_tiles_per_workgroup(hb, dev, oracle):
+    """Enough tiles that every workgroup walks many of them (register prefetch
+    of tile t+1 and the offsets of t+2 while t is hashed), with some tiles
+    over the LDS window in between (global fallback)."""
+    rng = np.random.default_rng(23)
+    n = 1_500_000
+    lens = rng.integers(0, 64, size=n)
+    lens[rng.integers(0, n, size=300)] = 5000  # a few tiles overflow the window
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    want = oracle.hash_var(data, off)
+    d_data, d_o = d_u8(data, dev), d_off(off, dev)
+    for k in VAR_KERNELS:
+        assert np.array_equal(u64(hb.hash_var(d_data, d_o, kernel=k)), want), k
+    # fixed lengths through the span kernel, many tiles per workgroup
+    flat = rng.integers(0, 256, size=2_000_000 * 37, dtype=np.uint8)
+    got = u64(hb.hash_fixed(d_u8(flat, dev), 37, kernel=4))
+    assert np.array_equal(got, oracle.hash_fixed(flat, 37))
+
+
 def test_var_long_keys(hb, dev, oracle):
     lens = np.array([65537, 1 << 20, 3, (1 << 20) + 15, 0, 100000], dtype=np.uint64)
     off = np.zeros(lens.size + 1, dtype=np.uint64)
@@ -197,9 +218,10 @@ def test_var_long_keys(hb, dev, oracle):
         assert np.array_equal(got, want), k
 
 
-def test_var_offsets_beyond_4gib(hb, dev, oracle):
-    """64-bit offsets: keys living past the first 4 GiB of the byte buffer."""
-    base = (1 << 32) + 12345
+@pytest.mark.parametrize("base", [(1 << 31) + 12345, (1 << 32) + 12345, (3 << 31) + 7])
+def test_var_offsets_beyond_2gib(hb, dev, oracle, base):
+    """64-bit offsets: keys living past 2 GiB / 4 GiB of the byte buffer, with
+    bit 31 of the low offset word set and clear (no sign extension anywhere)."""
     n = 2000
     rng = np.random.default_rng(3)
     lens = rng.integers(0, 300, size=n)
