@@ -102,3 +102,72 @@ double ref_bench_make_hash_loop(const uint8_t *keys, uint32_t key_len, uint64_t 
     free(args);
     return dt;
 }
+
+/* ---- drop-in check: GPU hashes through the reference's caller-supplied-hash
+ * seam (src/test.9.shf.c:176-182), read back through its own shf_make_hash().
+ *
+ * Reference API used (src/shf.h:373-437; SHF is opaque here):
+ *   shf_init, shf_attach, shf_set_is_lockable, shf_put_key_val,
+ *   shf_get_key_val_copy, shf_del; thread-locals shf_hash_key(_len),
+ *   shf_val, shf_val_len (src/shf.private.h:187-189, src/shf.h:363-364). */
+typedef struct SHF SHF;
+extern void shf_init(void);
+extern SHF *shf_attach(const char *path, const char *name, uint32_t delete_upon_process_exit);
+extern void shf_set_is_lockable(SHF *shf, uint32_t is_lockable);
+extern uint32_t shf_put_key_val(SHF *shf, const char *val, uint32_t val_len);
+extern uint32_t shf_get_key_val_copy(SHF *shf);
+extern uint32_t shf_del_key_val(SHF *shf);
+extern char *shf_del(SHF *shf);
+extern __thread const char *shf_hash_key;
+extern __thread uint32_t shf_hash_key_len;
+extern __thread char *shf_val;
+extern __thread uint32_t shf_val_len;
+
+#define REF_RET_KEY_FOUND 1u /* SHF_RET_KEY_FOUND, src/shf.h:345 */
+#define REF_RET_KEY_PUT 8u   /* SHF_RET_KEY_PUT,   src/shf.h:348 */
+
+/* The helper a maintainer adds next to shf_make_hash():
+ * install a precomputed SHF_HASH for `key` in the thread-local seam. */
+static void ref_use_hash(const char *key, uint32_t key_len, const uint64_t h[2])
+{
+    shf_hash.u64[0] = h[0];
+    shf_hash.u64[1] = h[1];
+    shf_hash_key = key;
+    shf_hash_key_len = key_len;
+}
+
+/* mode 0: put with the supplied hashes, get with the reference shf_make_hash();
+ * mode 1: put with shf_make_hash(), get and del with the supplied hashes.
+ * Returns the number of keys found with the right value (n when the supplied
+ * hashes equal the reference's), or -1 if the store could not be created. */
+int64_t ref_roundtrip_with_hashes(const char *folder, const char *name, const uint8_t *bytes,
+                                  const uint64_t *offsets, uint64_t n, const uint64_t *hashes, int mode)
+{
+    shf_init();
+    SHF *shf = shf_attach(folder, name, 0);
+    if (!shf) return -1;
+    shf_set_is_lockable(shf, 0);
+    int64_t good = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const char *k = (const char *)bytes + offsets[i];
+        const uint32_t kl = (uint32_t)(offsets[i + 1] - offsets[i]);
+        if (mode == 0) ref_use_hash(k, kl, hashes + 2 * i);
+        else shf_make_hash(k, kl);
+        if (shf_put_key_val(shf, (const char *)&i, sizeof(i)) != REF_RET_KEY_PUT) break;
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const char *k = (const char *)bytes + offsets[i];
+        const uint32_t kl = (uint32_t)(offsets[i + 1] - offsets[i]);
+        if (mode == 0) shf_make_hash(k, kl);
+        else ref_use_hash(k, kl, hashes + 2 * i);
+        if (shf_get_key_val_copy(shf) == REF_RET_KEY_FOUND && shf_val_len == sizeof(i) &&
+            memcmp(shf_val, &i, sizeof(i)) == 0)
+            ++good;
+        if (mode == 1) {
+            ref_use_hash(k, kl, hashes + 2 * i);
+            (void)shf_del_key_val(shf);
+        }
+    }
+    (void)shf_del(shf);
+    return good;
+}

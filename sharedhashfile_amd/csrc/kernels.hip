@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <atomic>
 
 #include "murmur3_mix.h"
@@ -153,71 +155,79 @@ __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ byt
 // while hashing round r out of LDS.
 // ---------------------------------------------------------------------------
 constexpr int kTileKeys = 64;
-constexpr int kRoundBlocks = 8;
 constexpr int kTiledWaves = 4;  // waves per workgroup
 
+// LDS slot of piece j of key k for R pieces (16 B each) per key per round. The
+// XOR term spreads the 16 lanes of each ds_read_b128 lane group (which always
+// hold 16 distinct values of k & 15) over 16 distinct 16-B bank slots.
+template <int R>
 __device__ __forceinline__ uint32_t tile_slot(uint32_t key, uint32_t piece) {
-  return key * (kRoundBlocks * 16) + 16u * (piece ^ ((key >> 1) & 7u));
+  constexpr uint32_t rows_per_bank_row = 16 / R;  // R=4: 4, R=8: 2, R=16: 1
+  return key * (R * 16) + 16u * (piece ^ ((key / rows_per_bank_row) & (R - 1)));
 }
 
-template <int OUT>
+template <int OUT, int R>
 __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __restrict__ keys, uint32_t key_len,
                                                             uint64_t n, uint32_t seed, void* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kTiledWaves][kTileKeys * kRoundBlocks * 16];
+  static_assert(R == 4 || R == 8 || R == 16, "pieces per key per round");
+  constexpr uint32_t kKeysPerInstr = 64 / R;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kTiledWaves][kTileKeys * R * 16];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   uint8_t* tile = lds[wave];
 
   const uint32_t nblocks = key_len >> 4;
-  const uint32_t rounds = (nblocks + kRoundBlocks - 1) / kRoundBlocks;
+  const uint32_t rounds = (nblocks + R - 1) / R;
   const uint64_t ntiles = (n + kTileKeys - 1) / kTileKeys;
   const uint64_t wstride = (uint64_t)gridDim.x * kTiledWaves;
   uint64_t t = (uint64_t)blockIdx.x * kTiledWaves + wave;
   if (t >= ntiles) return;
 
-  const uint32_t ld_key_sub = lane >> 3;  // + 8q
-  const uint32_t ld_piece = lane & 7u;
+  const uint32_t ld_key_sub = lane / R;  // + kKeysPerInstr * q
+  const uint32_t ld_piece = lane % R;
 
-  // Fetch round r of tile t into registers (8 x 16 B per lane).
-  auto fetch = [&](uint64_t tt, uint32_t r, u32x4 (&reg)[kRoundBlocks]) {
+  // Fetch round r of tile t into registers (R x 16 B per lane): instruction q
+  // reads kKeysPerInstr keys, R lanes per key covering 16R contiguous bytes.
+  auto fetch = [&](uint64_t tt, uint32_t r, u32x4 (&reg)[R]) {
     const uint64_t k0 = tt * kTileKeys;
-    const uint32_t rb = min((uint32_t)kRoundBlocks, nblocks - r * kRoundBlocks);
-    const bool full = rb == kRoundBlocks && k0 + kTileKeys <= n;
-    const uint8_t* src0 = keys + (k0 + ld_key_sub) * key_len + (uint64_t)r * 128u + 16u * ld_piece;
+    const uint32_t rb = min((uint32_t)R, nblocks - r * R);
+    const bool full = rb == (uint32_t)R && k0 + kTileKeys <= n;
+    const uint8_t* src0 = keys + (k0 + ld_key_sub) * key_len + (uint64_t)r * (16u * R) + 16u * ld_piece;
     if (full) {  // common case: no per-lane predicate
 #pragma unroll
-      for (int q = 0; q < kRoundBlocks; ++q)
-        reg[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src0 + (uint64_t)(8u * q) * key_len));
+      for (int q = 0; q < R; ++q)
+        reg[q] = __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4*>(src0 + (uint64_t)(kKeysPerInstr * q) * key_len));
     } else {
 #pragma unroll
-      for (int q = 0; q < kRoundBlocks; ++q) {
-        const uint64_t key = k0 + 8u * q + ld_key_sub;
-        reg[q] = (key < n && ld_piece < rb)
-                     ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src0 + (uint64_t)(8u * q) * key_len))
-                     : u32x4{0u, 0u, 0u, 0u};
+      for (int q = 0; q < R; ++q) {
+        const uint64_t key = k0 + kKeysPerInstr * q + ld_key_sub;
+        reg[q] = (key < n && ld_piece < rb) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                                                  src0 + (uint64_t)(kKeysPerInstr * q) * key_len))
+                                            : u32x4{0u, 0u, 0u, 0u};
       }
     }
   };
 
-  u32x4 nxt[kRoundBlocks];
+  u32x4 nxt[R];
   fetch(t, 0, nxt);
   uint32_t r = 0;
   State s{seed, seed};
   while (true) {
     // Stage the fetched round into LDS.
 #pragma unroll
-    for (int q = 0; q < kRoundBlocks; ++q)
-      *reinterpret_cast<u32x4*>(tile + tile_slot(8u * q + ld_key_sub, ld_piece)) = nxt[q];
+    for (int q = 0; q < R; ++q)
+      *reinterpret_cast<u32x4*>(tile + tile_slot<R>(kKeysPerInstr * q + ld_key_sub, ld_piece)) = nxt[q];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    const uint32_t rb = min((uint32_t)kRoundBlocks, nblocks - r * kRoundBlocks);
+    const uint32_t rb = min((uint32_t)R, nblocks - r * R);
     // Read this round's blocks of this lane's key (all reads in flight at once).
-    u32x4 b[kRoundBlocks];
+    u32x4 b[R];
 #pragma unroll
-    for (int j = 0; j < kRoundBlocks; ++j)
-      b[j] = ((uint32_t)j < rb) ? *reinterpret_cast<const u32x4*>(tile + tile_slot(lane, (uint32_t)j))
+    for (int j = 0; j < R; ++j)
+      b[j] = ((uint32_t)j < rb) ? *reinterpret_cast<const u32x4*>(tile + tile_slot<R>(lane, (uint32_t)j))
                                 : u32x4{0u, 0u, 0u, 0u};
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -234,7 +244,7 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
     if (more) fetch(t_next, r_next, nxt);
 
 #pragma unroll
-    for (int j = 0; j < kRoundBlocks; ++j)
+    for (int j = 0; j < R; ++j)
       if ((uint32_t)j < rb) body_block(s, pack64(b[j].x, b[j].y), pack64(b[j].z, b[j].w));
 
     if (r + 1 == rounds) {
@@ -420,7 +430,7 @@ __global__ __launch_bounds__(64) void k_span(const uint8_t* __restrict__ bytes, 
 // ---------------------------------------------------------------------------
 // Workgroups of `kernel` that fit on the whole device at once (cached per device).
 static unsigned resident_grid(const void* kernel, int block, size_t dyn_lds, int slot) {
-  static std::atomic<unsigned> cache[16][8];
+  static std::atomic<unsigned> cache[16][16];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
   unsigned g = cache[dev][slot].load(std::memory_order_relaxed);
@@ -432,6 +442,17 @@ static unsigned resident_grid(const void* kernel, int block, size_t dyn_lds, int
   g = (unsigned)(per_cu * cus);
   cache[dev][slot].store(g, std::memory_order_relaxed);
   return g;
+}
+
+// Pieces (16 B) of every key staged per round by k_tiled: 8 (one 128-B line per
+// key) unless SHF_HB_TILED_ROUND=4|16 overrides it (a tuning knob, read once).
+static int tiled_round_pieces() {
+  static const int r = [] {
+    const char* e = getenv("SHF_HB_TILED_ROUND");
+    const int v = e ? atoi(e) : 8;
+    return (v == 4 || v == 16) ? v : 8;
+  }();
+  return r;
 }
 
 static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
@@ -472,9 +493,16 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
     case kKernelTiled: {
       if (key_len < 32 || (key_len & 15u) || !al16) return hipErrorInvalidValue;
       const uint64_t tiles = (n + kTileKeys - 1) / kTileKeys;
-      const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_tiled<OUT>), 64 * kTiledWaves, 0, OUT);
-      hipLaunchKernelGGL(k_tiled<OUT>, dim3(grid_for(tiles, kTiledWaves, res)), dim3(64 * kTiledWaves), 0, st,
-                         reinterpret_cast<const uint8_t*>(keys), key_len, n, seed, out);
+      const int r = tiled_round_pieces();
+      const void* fn = r == 4    ? reinterpret_cast<const void*>(&k_tiled<OUT, 4>)
+                       : r == 16 ? reinterpret_cast<const void*>(&k_tiled<OUT, 16>)
+                                 : reinterpret_cast<const void*>(&k_tiled<OUT, 8>);
+      const unsigned res = resident_grid(fn, 64 * kTiledWaves, 0, 6 + OUT * 3 + (r == 4 ? 0 : r == 8 ? 1 : 2));
+      const dim3 g(grid_for(tiles, kTiledWaves, res)), b(64 * kTiledWaves);
+      const uint8_t* k8 = reinterpret_cast<const uint8_t*>(keys);
+      if (r == 4) hipLaunchKernelGGL((k_tiled<OUT, 4>), g, b, 0, st, k8, key_len, n, seed, out);
+      else if (r == 16) hipLaunchKernelGGL((k_tiled<OUT, 16>), g, b, 0, st, k8, key_len, n, seed, out);
+      else hipLaunchKernelGGL((k_tiled<OUT, 8>), g, b, 0, st, k8, key_len, n, seed, out);
       break;
     }
     case kKernelSpan:
