@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--keys256", type=int, default=100_000_000, help="configs[2]: 256-B keys per GPU")
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
     p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var (default: all)")
+    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic"])
+    p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
@@ -97,15 +99,17 @@ def make_workloads(args, dev, rank):
         n = args.keys16
         keys = device_random_bytes(n * 16, seed_base + 1, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        fk = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
         wl.append(Workload("fixed16", n, 16 + 16,
-                           lambda k=keys, o=out, n=n: hb.hash_fixed(k, 16, out=o),
+                           lambda k=keys, o=out, fk=fk: hb.hash_fixed(k, 16, out=o, kernel=fk),
                            "k_fixed16", "%d fixed 16-B keys" % n))
     if "fixed256" in only:
         n = args.keys256
         keys = device_random_bytes(n * 256, seed_base + 2, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        fk = {"auto": 0, "fixed16": 2, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
         wl.append(Workload("fixed256", n, 256 + 16,
-                           lambda k=keys, o=out: hb.hash_fixed(k, 256, out=o),
+                           lambda k=keys, o=out, fk=fk: hb.hash_fixed(k, 256, out=o, kernel=fk),
                            "k_tiled", "%d fixed 256-B keys" % n))
     if "var" in only:
         n = args.keysvar
@@ -119,8 +123,9 @@ def make_workloads(args, dev, rank):
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         del lens
         wl.append(Workload("var", n, total / n + 8 + 16,
-                           lambda d=data, o=off, out=out: hb.hash_var(d, o, out=out),
-                           "k_generic", "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
+                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3}[args.var_kernel]:
+                           hb.hash_var(d, o, out=out, kernel=vk),
+                           "k_span" if args.var_kernel != "generic" else "k_generic", "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
     torch.cuda.synchronize()
     return wl
 

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSV output: mean counter value per kernel.
+
+    python tools/pmc_summary.py <dir containing *counter_collection.csv> [kernel-substring ...]
+"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+
+def short(name):
+    name = name.split("(")[0]
+    return name.replace("void ", "").replace("shfhb::", "")
+
+
+def main():
+    root = sys.argv[1]
+    want = sys.argv[2:]
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                if want and not any(w in k for w in want):
+                    continue
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for k, cs in sorted(acc.items()):
+        print(k)
+        for c, v in sorted(cs.items()):
+            print("   %-28s %16.1f  (n=%d)" % (c, sum(v) / len(v), len(v)))
+
+
+if __name__ == "__main__":
+    main()
