@@ -34,12 +34,30 @@ struct State {
   uint64_t h1, h2;
 };
 
-// One 16-byte body block whose k1/k2 are already mixed (murmurhash3.c:97-103).
+// One 16-byte body block whose k1/k2 are already mixed (murmurhash3.c:97-103):
+//   h1 = (rotl(h1 ^ m1, 27) + h2) * 5 + N1
+//   h2 = (rotl(h2 ^ m2, 31) + h1) * 5 + N2
+// distributed (mod 2^64) as
+//   h1' = rotl(h1 ^ m1, 27) * 5 + (h2 * 5 + N1)
+//   h2' = rotl(h2 ^ m2, 31) * 5 + (h1' * 5 + N2)
+// so everything but `h1' * 5 + N2 + ...` is off the serial h1 -> h2 -> h1 path:
+// the chain across blocks is the latency bound of a lane, not its op count.
+#ifndef SHFHB_CHAIN_DISTRIBUTED
+#define SHFHB_CHAIN_DISTRIBUTED 1
+#endif
 __device__ __forceinline__ void chain_block(State& s, uint64_t m1, uint64_t m2) {
+#if SHFHB_CHAIN_DISTRIBUTED
+  const uint64_t a1 = rotl64(s.h1 ^ m1, 27) * 5;
+  const uint64_t b1 = s.h2 * 5 + kN1;
+  const uint64_t a2 = rotl64(s.h2 ^ m2, 31) * 5;
+  s.h1 = a1 + b1;
+  s.h2 = a2 + (s.h1 * 5 + kN2);
+#else
   s.h1 ^= m1;
   s.h1 = (rotl64(s.h1, 27) + s.h2) * 5 + kN1;
   s.h2 ^= m2;
   s.h2 = (rotl64(s.h2, 31) + s.h1) * 5 + kN2;
+#endif
 }
 
 __device__ __forceinline__ void body_block(State& s, uint64_t k1, uint64_t k2) {

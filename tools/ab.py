@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of library build variants in ONE process
+(cdna_hip_programming.md s5.4 rule 24).
+
+    python tools/ab.py --variant base= --variant nodist=-DSHFHB_CHAIN_DISTRIBUTED=0 \
+        --workload fixed256 --n 20000000 --rounds 8
+
+Each variant is the same sources built with extra -D flags into its own .so
+(loaded side by side through ctypes); every round times every variant once.
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def build(name, flags, outdir):
+    from sharedhashfile_amd import build as b
+
+    so = os.path.join(outdir, "lib_%s.so" % name)
+    cmd = [b.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+           "-I" + os.path.join(ROOT, "include")] + flags.split() + [os.path.join(b.CSRC, s) for s in b.SOURCES] + [
+               "-o", so]
+    subprocess.check_call(cmd)
+    return so
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--variant", action="append", required=True, help="name=-Dflags ...")
+    p.add_argument("--workload", default="fixed256", choices=["fixed16", "fixed256", "var", "fixedL"])
+    p.add_argument("--key-len", type=int, default=37)
+    p.add_argument("--n", type=int, default=20_000_000)
+    p.add_argument("--rounds", type=int, default=6)
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--kernel", type=int, default=0)
+    a = p.parse_args()
+
+    import torch
+
+    import sharedhashfile_amd as hb
+    from sharedhashfile_amd.keygen import device_random_bytes
+
+    outdir = tempfile.mkdtemp(prefix="shfhb_ab_")
+    libs = {}
+    for v in a.variant:
+        name, _, flags = v.partition("=")
+        libs[name] = hb.load(build(name, flags, outdir))
+    dev = torch.device("cuda:0")
+    n = a.n
+    if a.workload in ("fixed16", "fixed256", "fixedL"):
+        L = {"fixed16": 16, "fixed256": 256, "fixedL": a.key_len}[a.workload]
+        keys = device_random_bytes(n * L, 1, dev)
+        per_key = L + 16
+        call = lambda lib, out: lib.shf_hash_batch_fixed_kernel_async(keys.data_ptr(), L, n, 12345, out.data_ptr(),
+                                                                       a.kernel, None)
+    else:
+        g = torch.Generator(device=dev)
+        g.manual_seed(3)
+        lens = torch.randint(8, 513, (n,), generator=g, device=dev, dtype=torch.int64)
+        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=off[1:])
+        data = device_random_bytes(int(off[-1].item()), 2, dev)
+        per_key = float(off[-1].item()) / n + 24
+        call = lambda lib, out: lib.shf_hash_batch_var_kernel_async(data.data_ptr(), off.data_ptr(), n, 12345,
+                                                                     out.data_ptr(), a.kernel, None)
+    outs = {k: torch.empty((n, 2), dtype=torch.int64, device=dev) for k in libs}
+    for k, lib in libs.items():
+        assert call(lib, outs[k]) == 0
+    torch.cuda.synchronize()
+    ref = next(iter(outs.values()))
+    for k, o in outs.items():
+        assert torch.equal(o, ref), "variant %s differs" % k
+    times = {k: [] for k in libs}
+    for r in range(a.rounds):
+        for k, lib in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.reps):
+                call(lib, outs[k])
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) / a.reps)
+    for k, ts in times.items():
+        ts = sorted(ts)
+        med = ts[len(ts) // 2]
+        print("%-12s median %8.3f ms  min %8.3f ms  %7.1f GB/s  %6.2f Gkeys/s" % (
+            k, med, ts[0], n * per_key / med / 1e6, n / med / 1e6))
+
+
+if __name__ == "__main__":
+    main()

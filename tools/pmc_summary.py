@@ -22,9 +22,10 @@ def main():
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                k = short(row["Kernel_Name"])
-                if want and not any(w in k for w in want):
+                raw = row["Kernel_Name"]
+                if want and not any(w in raw for w in want):
                     continue
+                k = short(raw)
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, cs in sorted(acc.items()):
         print(k)
