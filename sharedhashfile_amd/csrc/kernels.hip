@@ -155,7 +155,10 @@ __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ byt
 // while hashing round r out of LDS.
 // ---------------------------------------------------------------------------
 constexpr int kTileKeys = 64;
-constexpr int kTiledWaves = 4;  // waves per workgroup
+#ifndef SHFHB_TILED_WAVES
+#define SHFHB_TILED_WAVES 4
+#endif
+constexpr int kTiledWaves = SHFHB_TILED_WAVES;  // waves per workgroup
 
 // LDS slot of piece j of key k for R pieces (16 B each) per key per round. The
 // XOR term spreads the 16 lanes of each ds_read_b128 lane group (which always
