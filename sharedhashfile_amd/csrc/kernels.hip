@@ -272,8 +272,10 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
 // at any byte). A tile whose span exceeds the LDS window is hashed straight
 // from global memory (wave-uniform fallback; rare for keys <= 320 B).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSpanCap = 20u * 1024u;      // LDS bytes per wave
-constexpr int kSpanPieces = kSpanCap / 1024u;   // 16-B pieces per lane per full span
+constexpr uint32_t kSpanAlloc = 20u * 1024u;                  // LDS bytes per wave (8 waves per CU)
+constexpr uint32_t kSpanPad = 64;                              // read slack past a staged span
+constexpr uint32_t kSpanCap = kSpanAlloc - kSpanPad;           // largest span staged in LDS
+constexpr int kSpanPieces = (kSpanCap + 1023u) / 1024u;        // 16-B pieces per lane per full span
 
 template <bool VAR>
 struct SpanTile {
@@ -341,38 +343,36 @@ __device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[kSp
     if ((uint32_t)q * 1024u < span16) reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
 }
 
-// Hash `len` bytes starting at byte offset p of the staged span. Only dwords
-// holding bytes of the key are read (plus none past the staged region).
+// Hash `len` bytes starting at byte offset p of the staged span. The next
+// block's dwords are read while the current block is mixed (LDS latency off the
+// critical path); reads may run up to kSpanPad bytes past the span, into the
+// window's padding, and such bytes are never used.
 __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
   const uint32_t sh = p & 3u;
   const uint32_t* w = lds + (p >> 2);
   const uint32_t nblocks = len >> 4;
   State s{seed, seed};
-  uint32_t x0 = (len > 0) ? w[0] : 0u;
+  uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
   for (uint32_t j = 0; j < nblocks; ++j) {
-    const uint32_t* v = w + 4 * j;
-    const uint32_t x1 = v[1], x2 = v[2], x3 = v[3];
-    const bool need4 = sh != 0 || j + 1 < nblocks || (len & 15u) != 0;
-    const uint32_t x4 = need4 ? v[4] : 0u;
+    const uint32_t* v = w + 4 * j + 4;
+    const uint32_t y1 = v[1], y2 = v[2], y3 = v[3], y4 = v[4];
     const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
     const uint32_t d1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
     const uint32_t d2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
     const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
     body_block(s, pack64(d0, d1), pack64(d2, d3));
     x0 = x4;
+    x1 = y1;
+    x2 = y2;
+    x3 = y3;
+    x4 = y4;
   }
   const uint32_t rem = len & 15u;
-  if (rem) {
-    const uint32_t* t = w + 4 * nblocks;
-    const uint32_t need = sh + rem;
-    uint32_t x[5];
-    x[0] = x0;
-#pragma unroll
-    for (int q = 1; q < 5; ++q) x[q] = (4u * q < need) ? t[q] : 0u;
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
-    const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
+  if (rem) {  // x0..x4 now hold the dwords of the tail
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
     const uint64_t t1 = pack64(d0, d1) & low_bytes_mask(rem);
     const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
     tail_block(s, t1, t2, rem);
@@ -469,9 +469,9 @@ template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
                               uint64_t n, uint32_t seed, void* out, hipStream_t st) {
   const uint64_t tiles = (n + 63) / 64;
-  const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR>), 64, kSpanCap,
+  const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR>), 64, kSpanAlloc,
                                      2 + OUT * 2 + (VAR ? 1 : 0));
-  hipLaunchKernelGGL((k_span<OUT, VAR>), dim3(grid_for(tiles, 1, res)), dim3(64), kSpanCap, st,
+  hipLaunchKernelGGL((k_span<OUT, VAR>), dim3(grid_for(tiles, 1, res)), dim3(64), kSpanAlloc, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, out);
   return hipGetLastError();
 }

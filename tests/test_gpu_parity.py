@@ -41,7 +41,7 @@ def fixed_kernels(key_len, aligned=True):
         ks.append(1)
     if key_len >= 32 and key_len % 16 == 0 and aligned:
         ks.append(2)
-    if key_len * 64 + 16 <= 20 * 1024:
+    if key_len * 64 + 16 <= 20 * 1024 - 64:
         ks.append(4)  # SPAN
     return ks
 
@@ -166,8 +166,9 @@ def test_var_span_edges(hb, dev, oracle):
     cases = [
         np.zeros(200, dtype=np.int64),                                 # every tile empty
         np.concatenate([np.zeros(64, np.int64), rng.integers(0, 40, 100)]),
-        np.full(64, 320, dtype=np.int64),                              # 20480 B: exactly the window (aligned)
-        np.full(64, 319, dtype=np.int64),
+        np.full(64, 319, dtype=np.int64),                              # 20416 B: exactly the window
+        np.full(64, 318, dtype=np.int64),
+        np.full(64, 320, dtype=np.int64),                              # just over: fallback
         np.full(130, 321, dtype=np.int64),                             # > window: fallback tiles
         np.concatenate([np.full(63, 1, np.int64), [20000], np.full(65, 7, np.int64)]),
         rng.integers(300, 340, size=1000),                             # straddles the window size
