@@ -31,6 +31,9 @@ namespace shfhb {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;          // global-memory views
+typedef __attribute__((address_space(1))) const u32x4_a4 g_u32x4_a4;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
 
 template <int OUT>
 __device__ __forceinline__ void store_result(void* __restrict__ out, uint64_t i, const State& s) {
@@ -70,13 +73,13 @@ __device__ __forceinline__ uint64_t low_bytes_mask(uint32_t nbytes) {
 __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint32_t seed) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
   const uint32_t sh = (uint32_t)(addr & 3u);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(addr - sh);
+  const g_u32* w = reinterpret_cast<const g_u32*>(addr - sh);
   const uint32_t nblocks = len >> 4;
   State s{seed, seed};
 
   uint32_t j = 0;
   for (; j + 4 <= nblocks; j += 4) {  // 64-B burst per lane
-    const u32x4_a4* v = reinterpret_cast<const u32x4_a4*>(w + 4 * j);
+    const g_u32x4_a4* v = reinterpret_cast<const g_u32x4_a4*>(w + 4 * j);
     const u32x4 a = v[0], b = v[1], c = v[2], d = v[3];
     const uint32_t e = sh ? w[4 * j + 16] : 0u;
     const uint32_t x[17] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e};
@@ -90,7 +93,7 @@ __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint
     }
   }
   for (; j < nblocks; ++j) {
-    const u32x4 a = *reinterpret_cast<const u32x4_a4*>(w + 4 * j);
+    const u32x4 a = *reinterpret_cast<const g_u32x4_a4*>(w + 4 * j);
     const uint32_t e = sh ? w[4 * j + 4] : 0u;
     const uint32_t d0 = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
     const uint32_t d1 = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
@@ -101,7 +104,7 @@ __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint
 
   const uint32_t rem = len & 15u;
   if (rem) {
-    const uint32_t* t = w + 4 * nblocks;
+    const g_u32* t = w + 4 * nblocks;
     const uint32_t need = sh + rem;  // bytes spanned from the aligned base
     uint32_t x[5];
 #pragma unroll
@@ -272,10 +275,13 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
 // at any byte). A tile whose span exceeds the LDS window is hashed straight
 // from global memory (wave-uniform fallback; rare for keys <= 320 B).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSpanAlloc = 20u * 1024u;                  // LDS bytes per wave (8 waves per CU)
-constexpr uint32_t kSpanPad = 64;                              // read slack past a staged span
-constexpr uint32_t kSpanCap = kSpanAlloc - kSpanPad;           // largest span staged in LDS
-constexpr int kSpanPieces = (kSpanCap + 1023u) / 1024u;        // 16-B pieces per lane per full span
+// LDS per wave (one wave per workgroup, 8 per CU): [0, kSpanCap) the staged
+// span, then kSpanPad bytes of read slack, then the deferred-tile list.
+constexpr uint32_t kSpanAlloc = 20u * 1024u;
+constexpr uint32_t kSpanPad = 64;
+constexpr uint32_t kSpanDefer = 128;                                        // deferred tiles per wave
+constexpr uint32_t kSpanCap = kSpanAlloc - kSpanPad - 4u * kSpanDefer;      // 19904 B
+constexpr int kSpanPiecesMax = (kSpanCap + 1023u) / 1024u;                  // 20
 
 template <bool VAR>
 struct SpanTile {
@@ -287,20 +293,43 @@ struct SpanTile {
   uint32_t span16;    // bytes to stage, multiple of 16 (uniform; > kSpanCap -> fallback)
 };
 
+// Raw per-lane offsets of a tile, loaded well before they are needed: the
+// span of tile t+2 is only computed (waited for) after tile t is hashed, so
+// these loads never make the wave wait for the prefetch of tile t+1 that was
+// issued before them (vmcnt retires in order).
+struct SpanRaw {
+  uint64_t t;
+  uint64_t o0, o1;
+};
+
 template <bool VAR>
-__device__ __forceinline__ SpanTile<VAR> span_tile(const uint8_t* bytes, const uint64_t* offsets, uint64_t off_base,
-                                                   uint32_t key_len, uint64_t n, uint64_t t, uint32_t lane) {
+__device__ __forceinline__ SpanRaw span_load(const uint64_t* offsets, uint64_t n, uint64_t t, uint32_t lane) {
+  SpanRaw r;
+  r.t = t;
+  r.o0 = r.o1 = 0;
+  if constexpr (VAR) {
+    const uint64_t key = t * 64u + lane;
+    if (key < n) {
+      r.o0 = offsets[key];
+      r.o1 = offsets[key + 1];
+    }
+  }
+  return r;
+}
+
+template <bool VAR>
+__device__ __forceinline__ SpanTile<VAR> span_finish(const uint8_t* bytes, uint64_t off_base, uint32_t key_len,
+                                                     uint64_t n, const SpanRaw& raw, uint32_t lane) {
   SpanTile<VAR> ti;
-  const uint64_t k0 = t * 64u;
+  const uint64_t k0 = raw.t * 64u;
   const uint32_t kn = (uint32_t)min<uint64_t>(64u, n - k0);
   ti.key = k0 + lane;
   ti.valid = lane < kn;
   uint64_t first, end;  // tile bytes [first, end) relative to `bytes` (wave-uniform)
   if constexpr (VAR) {
-    const uint64_t o0 = ti.valid ? offsets[ti.key] : 0, o1 = ti.valid ? offsets[ti.key + 1] : 0;
-    ti.start = o0 - off_base;
-    ti.len = (uint32_t)(o1 - o0);
-    const uint64_t e_rel = o1 - off_base;
+    ti.start = raw.o0 - off_base;
+    ti.len = (uint32_t)(raw.o1 - raw.o0);
+    const uint64_t e_rel = raw.o1 - off_base;
     // the readlane builtins return a signed int: widen through uint32_t, never sign-extend
     first = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ti.start) |
             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ti.start >> 32)) << 32);
@@ -325,21 +354,29 @@ __device__ __forceinline__ SpanTile<VAR> span_tile(const uint8_t* bytes, const u
 }
 
 // Fetch the span into registers: piece q of lane l covers bytes q*1024 + 16l.
-// Only 16-B pieces holding at least one byte of the tile are loaded, so no load
-// can touch a page the keys do not.
-__device__ __forceinline__ void span_fetch(u32x4 (&reg)[kSpanPieces], uint64_t base, uint32_t span16, uint32_t lane) {
-  const u32x4* src = reinterpret_cast<const u32x4*>(base) + lane;
+// Raw buffer loads through a descriptor whose range is exactly the span: the
+// pieces past its end return 0 without touching memory, so every fetch issues
+// the same PIECES loads with no predicate at all. With a fixed count of
+// in-order (buffer, not flat) loads and no other vector-memory loads in the
+// loop body, the compiler waits for each staged piece with a counted vmcnt
+// instead of draining the prefetch.
+template <int PIECES>
+__device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(span16);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
 #pragma unroll
-  for (int q = 0; q < kSpanPieces; ++q) {
-    const uint32_t off = (uint32_t)q * 1024u + lane * 16u;
-    if ((uint32_t)q * 1024u < span16) reg[q] = off < span16 ? __builtin_nontemporal_load(src + 64 * q) : u32x4{0, 0, 0, 0};
-  }
+  for (int q = 0; q < PIECES; ++q)
+    reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
-__device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[kSpanPieces], uint32_t span16,
+template <int PIECES>
+__device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[PIECES], uint32_t span16,
                                            uint32_t lane) {
 #pragma unroll
-  for (int q = 0; q < kSpanPieces; ++q)
+  for (int q = 0; q < PIECES; ++q)
     if ((uint32_t)q * 1024u < span16) reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
 }
 
@@ -381,50 +418,72 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
   return s;
 }
 
-template <int OUT, bool VAR>
+template <int OUT, bool VAR, int PIECES>
 __global__ __launch_bounds__(64) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
                                              void* __restrict__ out) {
+  static_assert(PIECES * 1024 <= (int)(kSpanCap + 1023), "window");
+  constexpr uint32_t kCap = PIECES * 1024u < kSpanCap ? PIECES * 1024u : kSpanCap;
   extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
+  uint32_t* deferred = span_lds + (kSpanAlloc - 4u * kSpanDefer) / 4u;
   const uint32_t lane = threadIdx.x;
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t stride = gridDim.x;
   uint64_t t = blockIdx.x;
   if (t >= ntiles) return;
+  uint32_t n_deferred = 0;  // wave-uniform
 
-  u32x4 reg[kSpanPieces];
-  SpanTile<VAR> cur = span_tile<VAR>(bytes, offsets, off_base, key_len, n, t, lane);
-  if (cur.span16 <= kSpanCap) span_fetch(reg, cur.base, cur.span16, lane);
+  u32x4 reg[PIECES];
+  SpanTile<VAR> cur = span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, t, lane), lane);
+  span_fetch<PIECES>(reg, cur.base, cur.span16 <= kCap ? cur.span16 : 0u, lane);
   uint64_t t_next = t + stride;
-  SpanTile<VAR> nxt{};
-  if (t_next < ntiles) nxt = span_tile<VAR>(bytes, offsets, off_base, key_len, n, t_next, lane);
+  SpanRaw nxt_raw = span_load<VAR>(offsets, n, t_next < ntiles ? t_next : t, lane);
 
+  // Main loop: only tiles whose span fits the LDS window are hashed here, so the
+  // loop body's vector-memory traffic is exactly: PIECES span loads (tile t+1),
+  // two offset loads (tile t+2) and the result stores. Larger tiles are listed
+  // and hashed straight from HBM after the loop.
   while (true) {
-    const bool staged = cur.span16 <= kSpanCap;
-    if (staged) span_stage(span_lds, reg, cur.span16, lane);
+    const bool staged = cur.span16 <= kCap;
+    if (staged) span_stage<PIECES>(span_lds, reg, cur.span16, lane);
+    else {
+      if (n_deferred < kSpanDefer && lane == 0) deferred[n_deferred] = (uint32_t)(t_next - stride);
+      ++n_deferred;
+    }
     __syncthreads();
-    // prefetch the next tile's span while this one is hashed
     const bool more = t_next < ntiles;
-    if (more && nxt.span16 <= kSpanCap) span_fetch(reg, nxt.base, nxt.span16, lane);
+    SpanTile<VAR> nxt{};
+    if (more) nxt = span_finish<VAR>(bytes, off_base, key_len, n, nxt_raw, lane);
+    // offsets of the tile after next go out before the span fetch, so nothing
+    // issued after the fetch is needed before the fetch itself is
     const uint64_t t_nn = t_next + stride;
-    SpanTile<VAR> nn{};
-    if (t_nn < ntiles) nn = span_tile<VAR>(bytes, offsets, off_base, key_len, n, t_nn, lane);
+    SpanRaw nn_raw = span_load<VAR>(offsets, n, t_nn < ntiles ? t_nn : t, lane);
+    span_fetch<PIECES>(reg, nxt.base, (more && nxt.span16 <= kCap) ? nxt.span16 : 0u, lane);
 
-    if (cur.valid) {
-      State s;
-      if (staged) {
-        const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + cur.start - cur.base);
-        s = hash_lds(span_lds, p, cur.len, seed);
-      } else {
-        s = hash_bytes(bytes + cur.start, cur.len, seed);
-      }
-      store_result<OUT>(out, cur.key, s);
+    if (staged && cur.valid) {
+      const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + cur.start - cur.base);
+      store_result<OUT>(out, cur.key, hash_lds(span_lds, p, cur.len, seed));
     }
     __syncthreads();
     if (!more) break;
     cur = nxt;
-    nxt = nn;
+    nxt_raw = nn_raw;
     t_next = t_nn;
+  }
+
+  // Tiles too large for the window: per-lane loads straight from HBM.
+  auto hash_direct = [&](uint64_t tt) {
+    const SpanTile<VAR> ti = span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, tt, lane), lane);
+    if (ti.valid) store_result<OUT>(out, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
+  };
+  if (n_deferred <= kSpanDefer) {
+    for (uint32_t i = 0; i < n_deferred; ++i) hash_direct(deferred[i]);
+  } else {  // list overflowed: walk this wave's tiles again
+    for (uint64_t tt = blockIdx.x; tt < ntiles; tt += stride) {
+      const SpanTile<VAR> ti =
+          span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, tt, lane), lane);
+      if (ti.span16 > kCap && ti.valid) store_result<OUT>(out, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
+    }
   }
 }
 
@@ -433,7 +492,7 @@ __global__ __launch_bounds__(64) void k_span(const uint8_t* __restrict__ bytes, 
 // ---------------------------------------------------------------------------
 // Workgroups of `kernel` that fit on the whole device at once (cached per device).
 static unsigned resident_grid(const void* kernel, int block, size_t dyn_lds, int slot) {
-  static std::atomic<unsigned> cache[16][16];
+  static std::atomic<unsigned> cache[16][32];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
   unsigned g = cache[dev][slot].load(std::memory_order_relaxed);
@@ -465,15 +524,27 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
   return (unsigned)g;
 }
 
+template <int OUT, bool VAR, int PIECES>
+static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
+                                uint64_t n, uint32_t seed, void* out, hipStream_t st, int slot) {
+  const uint64_t tiles = (n + 63) / 64;
+  const unsigned res =
+      resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR, PIECES>), 64, kSpanAlloc, slot);
+  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3(grid_for(tiles, 1, res)), dim3(64), kSpanAlloc, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, out);
+  return hipGetLastError();
+}
+
+// Pieces per lane per tile: enough for a fixed-length tile's span (64 keys +
+// up to 15 bytes of misalignment), the whole window for variable lengths.
 template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
                               uint64_t n, uint32_t seed, void* out, hipStream_t st) {
-  const uint64_t tiles = (n + 63) / 64;
-  const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR>), 64, kSpanAlloc,
-                                     2 + OUT * 2 + (VAR ? 1 : 0));
-  hipLaunchKernelGGL((k_span<OUT, VAR>), dim3(grid_for(tiles, 1, res)), dim3(64), kSpanAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, out);
-  return hipGetLastError();
+  const int base_slot = 12 + OUT * 6 + (VAR ? 3 : 0);
+  const uint64_t need = VAR ? kSpanCap : (uint64_t)key_len * 64u + 16u;
+  if (need <= 4096) return launch_span_p<OUT, VAR, 4>(bytes, offsets, off_base, key_len, n, seed, out, st, base_slot);
+  if (need <= 8192) return launch_span_p<OUT, VAR, 8>(bytes, offsets, off_base, key_len, n, seed, out, st, base_slot + 1);
+  return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, key_len, n, seed, out, st, base_slot + 2);
 }
 
 template <int OUT>

@@ -41,7 +41,7 @@ def fixed_kernels(key_len, aligned=True):
         ks.append(1)
     if key_len >= 32 and key_len % 16 == 0 and aligned:
         ks.append(2)
-    if key_len * 64 + 16 <= 20 * 1024 - 64:
+    if key_len * 64 + 16 <= 19904:
         ks.append(4)  # SPAN
     return ks
 
@@ -166,9 +166,9 @@ def test_var_span_edges(hb, dev, oracle):
     cases = [
         np.zeros(200, dtype=np.int64),                                 # every tile empty
         np.concatenate([np.zeros(64, np.int64), rng.integers(0, 40, 100)]),
-        np.full(64, 319, dtype=np.int64),                              # 20416 B: exactly the window
-        np.full(64, 318, dtype=np.int64),
-        np.full(64, 320, dtype=np.int64),                              # just over: fallback
+        np.full(64, 311, dtype=np.int64),                              # 19904 B: exactly the window
+        np.full(64, 310, dtype=np.int64),
+        np.full(64, 312, dtype=np.int64),                              # just over: deferred tile
         np.full(130, 321, dtype=np.int64),                             # > window: fallback tiles
         np.concatenate([np.full(63, 1, np.int64), [20000], np.full(65, 7, np.int64)]),
         rng.integers(300, 340, size=1000),                             # straddles the window size
@@ -206,6 +206,22 @@ def test_var_many_tiles_per_workgroup(hb, dev, oracle):
     flat = rng.integers(0, 256, size=2_000_000 * 37, dtype=np.uint8)
     got = u64(hb.hash_fixed(d_u8(flat, dev), 37, kernel=4))
     assert np.array_equal(got, oracle.hash_fixed(flat, 37))
+
+
+def test_var_deferred_list_overflow(hb, dev, oracle):
+    """More oversized tiles per workgroup than the 128-entry deferred list holds
+    (the kernel then re-walks its tiles), mixed with staged tiles."""
+    rng = np.random.default_rng(29)
+    n = 64 * 3000 * 4
+    lens = rng.integers(0, 40, size=n)
+    big = rng.random(n // 64) < 0.5  # half of the tiles get one 25 KB key
+    lens[np.nonzero(big)[0] * 64 + 5] = 25000
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    want = oracle.hash_var(data, off)
+    for k in VAR_KERNELS:
+        assert np.array_equal(u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k)), want), k
 
 
 def test_var_long_keys(hb, dev, oracle):
