@@ -135,25 +135,27 @@ def time_workload(w, steps, warmup, dist):
     kernel seconds from HIP events on the launch stream)."""
     import torch
 
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.current_stream()  # the stream every launch goes to (hb passes it to the library)
     for _ in range(warmup):
         w.launch()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    ev0.record(stream)
+    for _ in range(steps):
         w.launch()
-        e.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
     elapsed = t1 - t0
-    per_launch = sum(s.elapsed_time(e) for s, e in ev) / steps / 1e3
+    # HIP events bracketing the timed region on the launch stream: mean device
+    # time per launch, back-to-back kernels (inter-kernel gaps included)
+    per_launch = ev0.elapsed_time(ev1) / steps / 1e3
     if dist:
         t = torch.tensor([elapsed, per_launch], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
