@@ -372,38 +372,82 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
     reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
+// Stage the fetched pieces that hold span bytes. The per-lane bound matters:
+// the last piece's lanes past the span would otherwise write into the padding
+// and the deferred-tile list that follow the window.
 template <int PIECES>
 __device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[PIECES], uint32_t span16,
                                            uint32_t lane) {
 #pragma unroll
   for (int q = 0; q < PIECES; ++q)
-    if ((uint32_t)q * 1024u < span16) reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
+    if ((uint32_t)q * 1024u < span16 && (uint32_t)q * 1024u + lane * 16u < span16)
+      reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
 }
 
 // Hash `len` bytes starting at byte offset p of the staged span. The next
 // block's dwords are read while the current block is mixed (LDS latency off the
-// critical path); reads may run up to kSpanPad bytes past the span, into the
+// critical path); reads may run up to 36 (< kSpanPad) bytes past the span, into the
 // window's padding, and such bytes are never used.
+#ifndef SHFHB_LDS_PIPE2
+#define SHFHB_LDS_PIPE2 1
+#endif
+__device__ __forceinline__ void mix_dwords(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t x4,
+                                           uint32_t sh, uint64_t& m1, uint64_t& m2) {
+  const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+  const uint32_t d1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+  const uint32_t d2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+  const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+  m1 = mix_k1(pack64(d0, d1));
+  m2 = mix_k2(pack64(d2, d3));
+}
+
 __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
   const uint32_t sh = p & 3u;
   const uint32_t* w = lds + (p >> 2);
   const uint32_t nblocks = len >> 4;
   State s{seed, seed};
+#if SHFHB_LDS_PIPE2
+  // Software pipeline over blocks: iteration j runs the serial h1/h2 chain of
+  // block j beside the (independent, multiply-heavy) k1/k2 mixes of block j+1,
+  // and reads the dwords of block j+2.
+  uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4];
+  uint32_t b1 = w[5], b2 = w[6], b3 = w[7], b4 = w[8];
+  uint64_t m1, m2;
+  mix_dwords(a0, a1, a2, a3, a4, sh, m1, m2);
+  for (uint32_t j = 0; j < nblocks; ++j) {
+    const uint32_t* v = w + 4 * j + 8;
+    const uint32_t c1 = v[1], c2 = v[2], c3 = v[3], c4 = v[4];
+    uint64_t n1, n2;
+    mix_dwords(a4, b1, b2, b3, b4, sh, n1, n2);
+    chain_block(s, m1, m2);
+    m1 = n1;
+    m2 = n2;
+    a0 = a4;
+    a1 = b1;
+    a2 = b2;
+    a3 = b3;
+    a4 = b4;
+    b1 = c1;
+    b2 = c2;
+    b3 = c3;
+    b4 = c4;
+  }
+  uint32_t x0 = a0, x1 = a1, x2 = a2, x3 = a3, x4 = a4;
+#else
   uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
   for (uint32_t j = 0; j < nblocks; ++j) {
     const uint32_t* v = w + 4 * j + 4;
     const uint32_t y1 = v[1], y2 = v[2], y3 = v[3], y4 = v[4];
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
-    const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
-    body_block(s, pack64(d0, d1), pack64(d2, d3));
+    uint64_t m1, m2;
+    mix_dwords(x0, x1, x2, x3, x4, sh, m1, m2);
+    chain_block(s, m1, m2);
     x0 = x4;
     x1 = y1;
     x2 = y2;
     x3 = y3;
     x4 = y4;
   }
+#endif
   const uint32_t rem = len & 15u;
   if (rem) {  // x0..x4 now hold the dwords of the tail
     const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);

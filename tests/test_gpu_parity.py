@@ -224,6 +224,21 @@ def test_var_deferred_list_overflow(hb, dev, oracle):
         assert np.array_equal(u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k)), want), k
 
 
+def test_var_near_window_and_deferred_mixed(hb, dev, oracle):
+    """Many tiles per workgroup whose spans straddle the LDS window: staged
+    tiles that use the window's last 1 KiB piece interleaved with deferred ones
+    (the staged bytes must never reach the deferred-tile list)."""
+    rng = np.random.default_rng(31)
+    n = 64 * 30000
+    lens = rng.integers(300, 322, size=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    want = oracle.hash_var(data, off)
+    got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=4))
+    assert np.array_equal(got, want)
+
+
 def test_var_long_keys(hb, dev, oracle):
     lens = np.array([65537, 1 << 20, 3, (1 << 20) + 15, 0, 100000], dtype=np.uint64)
     off = np.zeros(lens.size + 1, dtype=np.uint64)
