@@ -384,13 +384,8 @@ __device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[PIE
       reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
 }
 
-// Hash `len` bytes starting at byte offset p of the staged span. The next
-// block's dwords are read while the current block is mixed (LDS latency off the
-// critical path); reads may run up to 36 (< kSpanPad) bytes past the span, into the
-// window's padding, and such bytes are never used.
-#ifndef SHFHB_LDS_PIPE2
-#define SHFHB_LDS_PIPE2 1
-#endif
+// The independent k1/k2 mixes (murmurhash3.c:97, :101) of the 16 bytes that
+// start `sh` bytes into dwords x0..x4.
 __device__ __forceinline__ void mix_dwords(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t x4,
                                            uint32_t sh, uint64_t& m1, uint64_t& m2) {
   const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
@@ -401,12 +396,14 @@ __device__ __forceinline__ void mix_dwords(uint32_t x0, uint32_t x1, uint32_t x2
   m2 = mix_k2(pack64(d2, d3));
 }
 
+// Hash `len` bytes starting at byte offset p of the staged span. Reads may run
+// up to 36 (< kSpanPad) bytes past the span, into the window's padding; such
+// bytes are never used.
 __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
   const uint32_t sh = p & 3u;
   const uint32_t* w = lds + (p >> 2);
   const uint32_t nblocks = len >> 4;
   State s{seed, seed};
-#if SHFHB_LDS_PIPE2
   // Software pipeline over blocks: iteration j runs the serial h1/h2 chain of
   // block j beside the (independent, multiply-heavy) k1/k2 mixes of block j+1,
   // and reads the dwords of block j+2.
@@ -433,21 +430,6 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
     b4 = c4;
   }
   uint32_t x0 = a0, x1 = a1, x2 = a2, x3 = a3, x4 = a4;
-#else
-  uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-  for (uint32_t j = 0; j < nblocks; ++j) {
-    const uint32_t* v = w + 4 * j + 4;
-    const uint32_t y1 = v[1], y2 = v[2], y3 = v[3], y4 = v[4];
-    uint64_t m1, m2;
-    mix_dwords(x0, x1, x2, x3, x4, sh, m1, m2);
-    chain_block(s, m1, m2);
-    x0 = x4;
-    x1 = y1;
-    x2 = y2;
-    x3 = y3;
-    x4 = y4;
-  }
-#endif
   const uint32_t rem = len & 15u;
   if (rem) {  // x0..x4 now hold the dwords of the tail
     const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
@@ -458,93 +440,6 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
     const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
     tail_block(s, t1, t2, rem);
   }
-  finish(s, len);
-  return s;
-}
-
-// Two-phase hashing of a staged tile (wave = 64 keys), removing the per-lane
-// length imbalance from the multiply-heavy part:
-//  A. block-parallel: the tile's T full 16-B blocks are numbered f = P_k + j
-//     (P = exclusive prefix sum of the keys' block counts); round r gives lane l
-//     block f = 64r + l, whatever key it belongs to, so every lane mixes a block
-//     every round. The mixed (k1', k2') pair is written in place to LDS at 16f:
-//     16f <= the block's own source offset (full blocks before it are no longer
-//     than the bytes before it), later rounds only read at >= 16*64(r+1), and a
-//     round issues all its reads before its writes, so no source is overwritten
-//     before it is read. Tails are read into registers before phase A.
-//  B. lane-per-key: the serial h1/h2 chain over the key's mixed blocks (cheap
-//     ops only), then tail, fmix and store.
-#ifndef SHFHB_SPAN_AB
-#define SHFHB_SPAN_AB 1
-#endif
-__device__ __forceinline__ uint32_t lds_u32(const uint32_t* lds, uint32_t byte) { return lds[byte >> 2]; }
-
-__device__ __forceinline__ State hash_tile_ab(uint32_t* lds, bool valid, uint32_t p, uint32_t len, uint32_t seed,
-                                              uint32_t lane) {
-  const uint32_t nb = valid ? (len >> 4) : 0u;
-  const uint32_t rem = valid ? (len & 15u) : 0u;
-  // tail bytes -> registers (phase A may overwrite them)
-  uint64_t t1 = 0, t2 = 0;
-  if (rem) {
-    const uint32_t q = p + 16u * nb, sh = q & 3u;
-    const uint32_t* w = lds + (q >> 2);
-    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
-    const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
-    t1 = pack64(d0, d1) & low_bytes_mask(rem);
-    t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
-  }
-  // exclusive prefix sum of block counts
-  uint32_t incl = nb;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= (uint32_t)d) incl += y;
-  }
-  const uint32_t P = incl - nb;
-  const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // tail reads before any M write
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-  // phase A
-  uint32_t k = 0;  // wave-uniform: first key that may own a block of this round
-  for (uint32_t base = 0; base < T; base += 64u) {
-    const uint32_t x = base + lane;
-    uint32_t src = 0;
-    while (k < 64u) {
-      const uint32_t Pk = __builtin_amdgcn_readlane(P, k);
-      if (Pk >= base + 64u) break;
-      const uint32_t nbk = __builtin_amdgcn_readlane(nb, k);
-      const uint32_t pk = __builtin_amdgcn_readlane(p, k);
-      if (x >= Pk && x < Pk + nbk) src = pk + 16u * (x - Pk);
-      if (Pk + nbk > base + 64u) break;  // continues into the next round
-      ++k;
-    }
-    if (x < T) {
-      const uint32_t sh = src & 3u;
-      const uint32_t* w = lds + (src >> 2);
-      uint64_t m1, m2;
-      mix_dwords(w[0], w[1], w[2], w[3], w[4], sh, m1, m2);
-      reinterpret_cast<u32x4*>(lds)[x] = u32x4{(uint32_t)m1, (uint32_t)(m1 >> 32), (uint32_t)m2, (uint32_t)(m2 >> 32)};
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-  // phase B
-  State s{seed, seed};
-  const u32x4* M = reinterpret_cast<const u32x4*>(lds) + P;
-  u32x4 cur = nb ? M[0] : u32x4{0, 0, 0, 0};
-  for (uint32_t j = 0; j < nb; ++j) {
-    const u32x4 nxt = (j + 1 < nb) ? M[j + 1] : u32x4{0, 0, 0, 0};
-    chain_block(s, pack64(cur.x, cur.y), pack64(cur.z, cur.w));
-    cur = nxt;
-  }
-  tail_block(s, t1, t2, rem);
   finish(s, len);
   return s;
 }
@@ -591,18 +486,10 @@ __global__ __launch_bounds__(64) void k_span(const uint8_t* __restrict__ bytes, 
     SpanRaw nn_raw = span_load<VAR>(offsets, n, t_nn < ntiles ? t_nn : t, lane);
     span_fetch<PIECES>(reg, nxt.base, (more && nxt.span16 <= kCap) ? nxt.span16 : 0u, lane);
 
-#if SHFHB_SPAN_AB
-    if (staged) {
-      const uint32_t p = cur.valid ? (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + cur.start - cur.base) : 0u;
-      const State st = hash_tile_ab(span_lds, cur.valid, p, cur.len, seed, lane);
-      if (cur.valid) store_result<OUT>(out, cur.key, st);
-    }
-#else
     if (staged && cur.valid) {
       const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + cur.start - cur.base);
       store_result<OUT>(out, cur.key, hash_lds(span_lds, p, cur.len, seed));
     }
-#endif
     __syncthreads();
     if (!more) break;
     cur = nxt;
