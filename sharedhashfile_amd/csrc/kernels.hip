@@ -162,6 +162,9 @@ constexpr int kTileKeys = 64;
 #define SHFHB_TILED_WAVES 1  // one wave per workgroup measured 4 % faster than 4 at 100M x 256 B
 #endif
 constexpr int kTiledWaves = SHFHB_TILED_WAVES;  // waves per workgroup
+#ifndef SHFHB_TILED_BATCH
+#define SHFHB_TILED_BATCH 8  // LDS blocks read per batch in k_tiled
+#endif
 
 // LDS slot of piece j of key k for R pieces (16 B each) per key per round. The
 // XOR term spreads the 16 lanes of each ds_read_b128 lane group (which always
@@ -176,6 +179,7 @@ template <int OUT, int R>
 __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __restrict__ keys, uint32_t key_len,
                                                             uint64_t n, uint32_t seed, void* __restrict__ out) {
   static_assert(R == 4 || R == 8 || R == 16, "pieces per key per round");
+  constexpr int kTiledBatch = SHFHB_TILED_BATCH < R ? SHFHB_TILED_BATCH : R;
   constexpr uint32_t kKeysPerInstr = 64 / R;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kTiledWaves][kTileKeys * R * 16];
   const uint32_t lane = threadIdx.x & 63u;
@@ -229,12 +233,17 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     const uint32_t rb = min((uint32_t)R, nblocks - r * R);
-    // Read this round's blocks of this lane's key (all reads in flight at once).
-    u32x4 b[R];
+    // Read this round's blocks of this lane's key, kTiledBatch at a time (all of
+    // a batch in flight at once; smaller batches trade ILP for VGPRs/occupancy).
+    u32x4 b[kTiledBatch];
+    auto read_batch = [&](int j0) {
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-      b[j] = ((uint32_t)j < rb) ? *reinterpret_cast<const u32x4*>(tile + tile_slot<R>(lane, (uint32_t)j))
-                                : u32x4{0u, 0u, 0u, 0u};
+      for (int j = 0; j < kTiledBatch; ++j)
+        b[j] = ((uint32_t)(j0 + j) < rb)
+                   ? *reinterpret_cast<const u32x4*>(tile + tile_slot<R>(lane, (uint32_t)(j0 + j)))
+                   : u32x4{0u, 0u, 0u, 0u};
+    };
+    read_batch(0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -250,8 +259,16 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
     if (more) fetch(t_next, r_next, nxt);
 
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-      if ((uint32_t)j < rb) body_block(s, pack64(b[j].x, b[j].y), pack64(b[j].z, b[j].w));
+    for (int j0 = 0; j0 < R; j0 += kTiledBatch) {
+      if (j0) read_batch(j0);
+#pragma unroll
+      for (int j = 0; j < kTiledBatch; ++j)
+        if ((uint32_t)(j0 + j) < rb) body_block(s, pack64(b[j].x, b[j].y), pack64(b[j].z, b[j].w));
+    }
+    // every lane's reads of this round precede the next round's staging writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     if (r + 1 == rounds) {
       const uint64_t key = t * kTileKeys + lane;
