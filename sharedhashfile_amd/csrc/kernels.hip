@@ -596,9 +596,15 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   const unsigned cap = 256u * 32u;
   const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
   if (kernel == kKernelAuto) {
+    // Measured on MI355X, 6.4 GB batches (tools/sweep_fixed.sh, profiles/r1):
+    //  - k_tiled wins when every round is full (key_len a multiple of 128 B);
+    //  - k_span wins for lengths whose 64-key tiles fit its LDS window, except
+    //    multiples of 64 B, whose lane-per-key LDS reads all hit the same banks;
+    //  - short keys (< 48 B) and the rest: per-lane loads (k_generic).
     if (key_len == 16 && al16) kernel = kKernelFixed16;
-    else if (key_len >= 32 && (key_len & 15u) == 0 && al16) kernel = kKernelTiled;
-    else if ((uint64_t)key_len * 64u + 16u <= kSpanCap) kernel = kKernelSpan;
+    else if (key_len >= 128 && (key_len & 127u) == 0 && al16) kernel = kKernelTiled;
+    else if (key_len >= 48 && (key_len & 63u) != 0 && (uint64_t)key_len * 64u + 16u <= kSpanCap)
+      kernel = kKernelSpan;
     else kernel = kKernelGeneric;
   }
   switch (kernel) {
