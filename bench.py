@@ -59,6 +59,8 @@ def parse():
                    help="auto: at N=1 run two short rocprofv3 --pmc child passes for HBM bytes")
     p.add_argument("--host-inclusive", action="store_true",
                    help="also time the pinned host->device->host path (reported, never `value`)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="backend for the barrier/max-reduce only (gloo: multi-rank rehearsal on one GPU)")
     p.add_argument("--quiet", action="store_true")
     return p.parse_args()
 
@@ -157,7 +159,8 @@ def time_workload(w, steps, warmup, dist):
     # time per launch, back-to-back kernels (inter-kernel gaps included)
     per_launch = ev0.elapsed_time(ev1) / steps / 1e3
     if dist:
-        t = torch.tensor([elapsed, per_launch], dtype=torch.float64, device="cuda")
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed, per_launch], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, per_launch = float(t[0]), float(t[1])
     return elapsed, per_launch
@@ -273,13 +276,17 @@ def main():
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (HIP); none visible")
+    local = local % max(1, torch.cuda.device_count())  # ranks beyond the visible GPUs share them (rehearsal)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as tdist
 
-        tdist.init_process_group("nccl", device_id=dev)  # RCCL: barriers + one max-reduce, no data path
+        if args.dist_backend == "nccl":  # RCCL: barriers + one max-reduce, no data path
+            tdist.init_process_group("nccl", device_id=dev)
+        else:
+            tdist.init_process_group("gloo")
         dist = tdist
     hb.check_device()
 
