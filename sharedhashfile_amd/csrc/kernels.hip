@@ -48,11 +48,32 @@ __device__ __forceinline__ void store_result(void* __restrict__ out, uint64_t i,
 // ---------------------------------------------------------------------------
 // key_len == 16
 // ---------------------------------------------------------------------------
+#ifndef SHFHB_F16_UNROLL
+#define SHFHB_F16_UNROLL 1  // keys per lane per grid-stride step
+#endif
+#ifndef SHFHB_F16_GRID_CAP
+#define SHFHB_F16_GRID_CAP (256u * 32u)
+#endif
 template <int OUT>
 __global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
                                                  void* __restrict__ out) {
+  constexpr int U = SHFHB_F16_UNROLL;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // U keys per lane at a stride of the grid: U coalesced 16-B loads in flight
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    u32x4 k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) k[u] = __builtin_nontemporal_load(&keys[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      State s{seed, seed};
+      body_block(s, pack64(k[u].x, k[u].y), pack64(k[u].z, k[u].w));
+      finish(s, 16);
+      store_result<OUT>(out, i + u * stride, s);
+    }
+  }
+  for (; i < n; i += stride) {
     const u32x4 k = __builtin_nontemporal_load(&keys[i]);
     State s{seed, seed};
     body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
@@ -610,7 +631,7 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   switch (kernel) {
     case kKernelFixed16:
       if (key_len != 16 || !al16) return hipErrorInvalidValue;
-      hipLaunchKernelGGL(k_fixed16<OUT>, dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+      hipLaunchKernelGGL(k_fixed16<OUT>, dim3(grid_for(n, 256, SHFHB_F16_GRID_CAP)), dim3(256), 0, st,
                          reinterpret_cast<const u32x4*>(keys), n, seed, out);
       break;
     case kKernelTiled: {

@@ -40,6 +40,7 @@ def main():
     p.add_argument("--rounds", type=int, default=6)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--kernel", type=int, default=0)
+    p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
     a = p.parse_args()
 
     import torch
@@ -77,6 +78,14 @@ def main():
     ref = next(iter(outs.values()))
     for k, o in outs.items():
         assert torch.equal(o, ref), "variant %s differs" % k
+    if a.copy_ref:  # a known-good streaming reference on the same device: bytes in == bytes out
+        half = int(n * per_key) // 2
+        src_c = torch.empty(half, dtype=torch.uint8, device=dev)
+        dst_c = torch.empty_like(src_c)
+        libs["copy_ref"] = None
+        outs["copy_ref"] = None
+        call_orig = call
+        call = lambda lib, out: (dst_c.copy_(src_c), 0)[1] if lib is None else call_orig(lib, out)
     times = {k: [] for k in libs}
     for r in range(a.rounds):
         for k, lib in libs.items():
