@@ -154,17 +154,48 @@ int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys) {
   return SHF_HB_OK;
 }
 
+// Caller host memory that is already page-locked (hipHostMalloc /
+// hipHostRegister): DMA straight from / into it, no staging copy.
+bool is_host_pinned(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: clear the sticky error
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// memcpy split over a few threads: one core cannot keep up with PCIe.
+void par_memcpy(void* dst, const void* src, size_t n) {
+  constexpr size_t kMinPerThread = (size_t)4 << 20;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t t = std::min<size_t>({(size_t)8, (size_t)hw, std::max<size_t>(1, n / kMinPerThread)});
+  if (t <= 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n + t - 1) / t;
+  for (size_t i = 1; i < t; ++i) {
+    const size_t a = i * per, b = std::min(n, a + per);
+    if (a < b) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+  }
+  memcpy(dst, src, std::min(n, per));
+  for (auto& x : th) x.join();
+}
+
 // One chunk in flight per slot; `pending` remembers where its results go.
 struct Pending {
   bool busy = false;
-  shf_hash128* dst = nullptr;
+  shf_hash128* dst = nullptr;  // nullptr: results were DMA'd straight to the caller
   uint64_t count = 0;
 };
 
 int drain_slot(DevCtx* c, int s, Pending& p) {
   if (!p.busy) return SHF_HB_OK;
   HB_TRY(hipEventSynchronize(c->done[s]));
-  memcpy(p.dst, c->h_out[s], p.count * sizeof(shf_hash128));
+  if (p.dst) par_memcpy(p.dst, c->h_out[s], p.count * sizeof(shf_hash128));
   p.busy = false;
   return SHF_HB_OK;
 }
@@ -177,6 +208,7 @@ int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
   const uint64_t per = key_len ? std::max<uint64_t>(1, kStageBytes / key_len) : (uint64_t)1 << 22;
   const uint64_t chunk = std::min<uint64_t>(per, n);
   if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk))) return rc;
+  const bool in_pinned = is_host_pinned(keys), out_pinned = is_host_pinned(out);
   Pending pend[kSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += chunk, ++idx) {
@@ -184,13 +216,15 @@ int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
     const uint64_t cnt = std::min(chunk, n - i0);
     const size_t nb = (size_t)cnt * key_len;
-    if (nb) memcpy(c->h_in[s], keys + i0 * key_len, nb);
-    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], c->h_in[s], nb, hipMemcpyHostToDevice, c->st[s]));
+    const uint8_t* src = in_pinned ? keys + i0 * key_len : c->h_in[s];
+    if (nb && !in_pinned) par_memcpy(c->h_in[s], keys + i0 * key_len, nb);
+    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], src, nb, hipMemcpyHostToDevice, c->st[s]));
     HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, c->d_out[s], shfhb::kOutHash, c->st[s],
                                shfhb::kKernelAuto));
-    HB_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128), hipMemcpyDeviceToHost, c->st[s]));
+    HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
+                          hipMemcpyDeviceToHost, c->st[s]));
     HB_TRY(hipEventRecord(c->done[s], c->st[s]));
-    pend[s] = Pending{true, out + i0, cnt};
+    pend[s] = Pending{true, out_pinned ? nullptr : out + i0, cnt};
   }
   for (int s = 0; s < kSlots; ++s)
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
@@ -204,6 +238,7 @@ int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t
   int rc = current_ctx(&c);
   if (rc) return rc;
   const uint64_t max_keys = std::min<uint64_t>(n, (uint64_t)1 << 22);
+  const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets), out_pinned = is_host_pinned(out);
   Pending pend[kSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
@@ -231,14 +266,20 @@ int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t
     }
     const int s = (int)(idx % kSlots);
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
-    if (nb) memcpy(c->h_in[s], bytes + base, nb);
-    memcpy(c->h_off[s], offsets + i0, (cnt + 1) * sizeof(uint64_t));
-    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], c->h_in[s], nb, hipMemcpyHostToDevice, c->st[s]));
-    HB_TRY(hipMemcpyAsync(c->d_off[s], c->h_off[s], (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
+    if (nb && !in_pinned) par_memcpy(c->h_in[s], bytes + base, nb);
+    const uint64_t* off_src = offsets + i0;
+    if (!off_pinned) {
+      par_memcpy(c->h_off[s], offsets + i0, (cnt + 1) * sizeof(uint64_t));
+      off_src = c->h_off[s];
+    }
+    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], in_pinned ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
+                                  c->st[s]));
+    HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
     HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, c->d_out[s], shfhb::kOutHash, c->st[s]));
-    HB_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128), hipMemcpyDeviceToHost, c->st[s]));
+    HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
+                          hipMemcpyDeviceToHost, c->st[s]));
     HB_TRY(hipEventRecord(c->done[s], c->st[s]));
-    pend[s] = Pending{true, out + i0, cnt};
+    pend[s] = Pending{true, out_pinned ? nullptr : out + i0, cnt};
     i0 = i1;
   }
   for (int s = 0; s < kSlots; ++s)

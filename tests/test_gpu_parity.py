@@ -326,6 +326,27 @@ def test_host_var_multi_chunk(hb, dev, oracle):
     assert np.array_equal(hb.hash_var_host(data, off, n_devices=0), want)
 
 
+def test_host_pinned_buffers(hb, dev, oracle):
+    """Caller buffers already page-locked: DMA'd directly (no staging copy)."""
+    lib = hb.load()
+    n = 3_000_000
+    keys = torch.randint(0, 256, (n * 16,), dtype=torch.uint8).pin_memory()
+    out = torch.zeros((n, 2), dtype=torch.int64).pin_memory()
+    rc = lib.shf_hash_batch_fixed(keys.data_ptr(), 16, n, 12345, out.data_ptr(), hb.MEM_HOST)
+    assert rc == 0
+    assert np.array_equal(out.numpy().view(np.uint64), oracle.hash_fixed(keys.numpy(), 16, threads=8))
+    rng = np.random.default_rng(13)
+    m = 200_000
+    lens = rng.integers(0, 600, size=m)
+    off = torch.zeros(m + 1, dtype=torch.int64).pin_memory()
+    off[1:] = torch.from_numpy(np.cumsum(lens))
+    data = torch.randint(0, 256, (int(off[-1]),), dtype=torch.uint8).pin_memory()
+    out2 = torch.zeros((m, 2), dtype=torch.int64).pin_memory()
+    rc = lib.shf_hash_batch_var(data.data_ptr(), off.data_ptr(), m, 12345, out2.data_ptr(), hb.MEM_HOST)
+    assert rc == 0
+    assert np.array_equal(out2.numpy().view(np.uint64), oracle.hash_var(data.numpy(), off.numpy().view(np.uint64)))
+
+
 def test_host_huge_single_key(hb, dev, oracle):
     n_big = (70 << 20) + 9  # one key larger than a staging chunk
     data = np.frombuffer(splitmix_bytes(n_big + 100, 5), dtype=np.uint8)
