@@ -49,10 +49,10 @@ __device__ __forceinline__ void store_result(void* __restrict__ out, uint64_t i,
 // key_len == 16
 // ---------------------------------------------------------------------------
 #ifndef SHFHB_F16_UNROLL
-#define SHFHB_F16_UNROLL 1  // keys per lane per grid-stride step
+#define SHFHB_F16_UNROLL 1  // keys per lane per grid-stride step (2 and 4 measured no better)
 #endif
-#ifndef SHFHB_F16_GRID_CAP
-#define SHFHB_F16_GRID_CAP (256u * 32u)
+#ifndef SHFHB_F16_GRID_CAP  // one key per lane up to 2^28 keys: 6.36 vs 5.16 TB/s at 100M keys
+#define SHFHB_F16_GRID_CAP (1u << 20)  // against a 8192-block grid-stride loop (profiles/r1/ab_fixed16.txt)
 #endif
 template <int OUT>
 __global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
