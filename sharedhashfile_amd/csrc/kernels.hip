@@ -142,6 +142,9 @@ __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint
   return s;
 }
 
+#ifndef SHFHB_GENERIC_GRID_CAP
+#define SHFHB_GENERIC_GRID_CAP (256u * 32u)
+#endif
 template <int OUT, bool VAR>
 __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ bytes,
                                                  const uint64_t* __restrict__ offsets, uint64_t off_base,
@@ -183,6 +186,9 @@ constexpr int kTileKeys = 64;
 #define SHFHB_TILED_WAVES 1  // one wave per workgroup measured 4 % faster than 4 at 100M x 256 B
 #endif
 constexpr int kTiledWaves = SHFHB_TILED_WAVES;  // waves per workgroup
+#ifndef SHFHB_TILED_GRID_MULT
+#define SHFHB_TILED_GRID_MULT 1  // grid = this many x the resident workgroups (0: one tile per wave)
+#endif
 #ifndef SHFHB_TILED_BATCH
 #define SHFHB_TILED_BATCH 8  // LDS blocks read per batch in k_tiled
 #endif
@@ -642,7 +648,8 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
                        : r == 16 ? reinterpret_cast<const void*>(&k_tiled<OUT, 16>)
                                  : reinterpret_cast<const void*>(&k_tiled<OUT, 8>);
       const unsigned res = resident_grid(fn, 64 * kTiledWaves, 0, 6 + OUT * 3 + (r == 4 ? 0 : r == 8 ? 1 : 2));
-      const dim3 g(grid_for(tiles, kTiledWaves, res)), b(64 * kTiledWaves);
+      const dim3 g(grid_for(tiles, kTiledWaves, SHFHB_TILED_GRID_MULT ? res * SHFHB_TILED_GRID_MULT : 0xffffffffu)),
+          b(64 * kTiledWaves);
       const uint8_t* k8 = reinterpret_cast<const uint8_t*>(keys);
       if (r == 4) hipLaunchKernelGGL((k_tiled<OUT, 4>), g, b, 0, st, k8, key_len, n, seed, out);
       else if (r == 16) hipLaunchKernelGGL((k_tiled<OUT, 16>), g, b, 0, st, k8, key_len, n, seed, out);
@@ -652,7 +659,7 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
     case kKernelSpan:
       return launch_span<OUT, false>(keys, nullptr, 0, key_len, n, seed, out, st);
     default:
-      hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+      hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                          reinterpret_cast<const uint8_t*>(keys), (const uint64_t*)nullptr, (uint64_t)0, key_len, n,
                          seed, out);
       break;
@@ -665,7 +672,7 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
                                uint32_t seed, void* out, hipStream_t st, int kernel) {
   if (kernel == kKernelGeneric) {
     const unsigned cap = 256u * 32u;
-    hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, cap)), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, out);
     return hipGetLastError();
   }
