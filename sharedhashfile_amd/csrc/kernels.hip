@@ -620,7 +620,6 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
 template <int OUT>
 static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out,
                                  hipStream_t st, int kernel) {
-  const unsigned cap = 256u * 32u;
   const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
   if (kernel == kKernelAuto) {
     // Measured on MI355X, 6.4 GB batches (tools/sweep_fixed.sh, profiles/r1):
@@ -671,7 +670,6 @@ template <int OUT>
 static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
                                uint32_t seed, void* out, hipStream_t st, int kernel) {
   if (kernel == kKernelGeneric) {
-    const unsigned cap = 256u * 32u;
     hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, out);
     return hipGetLastError();
