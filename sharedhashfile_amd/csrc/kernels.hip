@@ -143,7 +143,7 @@ __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint
 }
 
 #ifndef SHFHB_GENERIC_GRID_CAP
-#define SHFHB_GENERIC_GRID_CAP (256u * 32u)
+#define SHFHB_GENERIC_GRID_CAP (1u << 20)  // one key per lane: 5.57 vs 5.19 TB/s at 32-B keys
 #endif
 template <int OUT, bool VAR>
 __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ bytes,
@@ -187,7 +187,8 @@ constexpr int kTileKeys = 64;
 #endif
 constexpr int kTiledWaves = SHFHB_TILED_WAVES;  // waves per workgroup
 #ifndef SHFHB_TILED_GRID_MULT
-#define SHFHB_TILED_GRID_MULT 1  // grid = this many x the resident workgroups (0: one tile per wave)
+#define SHFHB_TILED_GRID_MULT 0  // grid = this many x the resident workgroups (0: one tile per wave;
+                                 // 6.09 vs 5.05 TB/s at 100M x 256 B, profiles/r1/ab_tiled_grid.txt)
 #endif
 #ifndef SHFHB_TILED_BATCH
 #define SHFHB_TILED_BATCH 8  // LDS blocks read per batch in k_tiled
@@ -594,13 +595,17 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
   return (unsigned)g;
 }
 
+#ifndef SHFHB_SPAN_GRID_MULT
+#define SHFHB_SPAN_GRID_MULT 1  // grid = this many x the resident workgroups (0: one tile per wave)
+#endif
 template <int OUT, bool VAR, int PIECES>
 static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
                                 uint64_t n, uint32_t seed, void* out, hipStream_t st, int slot) {
   const uint64_t tiles = (n + 63) / 64;
   const unsigned res =
       resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR, PIECES>), 64, kSpanAlloc, slot);
-  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3(grid_for(tiles, 1, res)), dim3(64), kSpanAlloc, st,
+  const unsigned cap = SHFHB_SPAN_GRID_MULT ? res * SHFHB_SPAN_GRID_MULT : 0xffffffffu;
+  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3(grid_for(tiles, 1, cap)), dim3(64), kSpanAlloc, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, out);
   return hipGetLastError();
 }
