@@ -312,21 +312,25 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
 
 // ---------------------------------------------------------------------------
 // Span kernel: variable-length keys (offset array) and fixed lengths the tiled
-// kernel cannot take. One wave (= one workgroup) owns a tile of 64 consecutive
-// keys, whose bytes are one contiguous span of the packed buffer. The span is
-// fetched with fully coalesced 16-B loads (1 KiB per wave instruction) into
-// registers one tile ahead, staged in LDS, and each lane then hashes its own
-// key out of LDS with dword reads funnel-shifted by v_alignbyte_b32 (keys start
-// at any byte). A tile whose span exceeds the LDS window is hashed straight
-// from global memory (wave-uniform fallback; rare for keys <= 320 B).
+// kernel does not take. One wave (= one workgroup) owns a tile of 64
+// consecutive keys, whose bytes are one contiguous span of the packed buffer.
+// The span is fetched with fully coalesced 16-B raw buffer loads (1 KiB per
+// wave instruction) into registers, staged in LDS, and each lane then hashes
+// its own key out of LDS with dword reads funnel-shifted by v_alignbyte_b32
+// (keys start at any byte). A tile whose span exceeds the LDS window is hashed
+// straight from HBM (wave-uniform fallback; rare for keys <= 311 B).
+// One tile per workgroup and as many workgroups as tiles: the hardware
+// dispatcher keeps every CU's LDS full of tiles in flight, which measured
+// faster than a persistent grid with a one-tile-ahead register prefetch
+// (4.42 vs 4.05 TB/s on config D, profiles/r1/ab_span_grid.txt).
 // ---------------------------------------------------------------------------
-// LDS per wave (one wave per workgroup, 8 per CU): [0, kSpanCap) the staged
-// span, then kSpanPad bytes of read slack, then the deferred-tile list.
-constexpr uint32_t kSpanAlloc = 20u * 1024u;
+// LDS per workgroup: [0, span) the staged span, then kSpanPad bytes of read
+// slack. Variable-length launches take the full window; fixed-length launches
+// only what one tile's span needs, so more tiles fit a CU.
+constexpr uint32_t kSpanAlloc = 20u * 1024u;                    // 8 workgroups per CU
 constexpr uint32_t kSpanPad = 64;
-constexpr uint32_t kSpanDefer = 128;                                        // deferred tiles per wave
-constexpr uint32_t kSpanCap = kSpanAlloc - kSpanPad - 4u * kSpanDefer;      // 19904 B
-constexpr int kSpanPiecesMax = (kSpanCap + 1023u) / 1024u;                  // 20
+constexpr uint32_t kSpanCap = kSpanAlloc - kSpanPad;            // 20416 B
+constexpr int kSpanPiecesMax = (kSpanCap + 1023u) / 1024u;      // 20
 
 template <bool VAR>
 struct SpanTile {
@@ -338,10 +342,8 @@ struct SpanTile {
   uint32_t span16;    // bytes to stage, multiple of 16 (uniform; > kSpanCap -> fallback)
 };
 
-// Raw per-lane offsets of a tile, loaded well before they are needed: the
-// span of tile t+2 is only computed (waited for) after tile t is hashed, so
-// these loads never make the wave wait for the prefetch of tile t+1 that was
-// issued before them (vmcnt retires in order).
+// Raw per-lane offsets of a tile (variable lengths); span_finish turns them
+// into the tile's wave-uniform span.
 struct SpanRaw {
   uint64_t t;
   uint64_t o0, o1;
@@ -399,12 +401,9 @@ __device__ __forceinline__ SpanTile<VAR> span_finish(const uint8_t* bytes, uint6
 }
 
 // Fetch the span into registers: piece q of lane l covers bytes q*1024 + 16l.
-// Raw buffer loads through a descriptor whose range is exactly the span: the
-// pieces past its end return 0 without touching memory, so every fetch issues
-// the same PIECES loads with no predicate at all. With a fixed count of
-// in-order (buffer, not flat) loads and no other vector-memory loads in the
-// loop body, the compiler waits for each staged piece with a counted vmcnt
-// instead of draining the prefetch.
+// Raw buffer loads through a descriptor whose range is exactly the span: lanes
+// past its end get 0 without touching memory, so no per-lane predicate, and no
+// load can reach a page the span does not.
 template <int PIECES>
 __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
@@ -414,12 +413,12 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
       reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
 #pragma unroll
   for (int q = 0; q < PIECES; ++q)
-    reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
+    if ((uint32_t)q * 1024u < nb)
+      reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
-// Stage the fetched pieces that hold span bytes. The per-lane bound matters:
-// the last piece's lanes past the span would otherwise write into the padding
-// and the deferred-tile list that follow the window.
+// Stage the fetched pieces that hold span bytes (lanes past the span's end
+// write nothing: the window may be exactly the span plus its read slack).
 template <int PIECES>
 __device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[PIECES], uint32_t span16,
                                            uint32_t lane) {
@@ -490,71 +489,24 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
 }
 
 template <int OUT, bool VAR, int PIECES>
-__global__ __launch_bounds__(64) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
+__global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
-                                             void* __restrict__ out) {
-  static_assert(PIECES * 1024 <= (int)(kSpanCap + 1023), "window");
-  constexpr uint32_t kCap = PIECES * 1024u < kSpanCap ? PIECES * 1024u : kSpanCap;
+                                             uint32_t cap, void* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  uint32_t* deferred = span_lds + (kSpanAlloc - 4u * kSpanDefer) / 4u;
   const uint32_t lane = threadIdx.x;
-  const uint64_t ntiles = (n + 63) / 64;
-  const uint64_t stride = gridDim.x;
-  uint64_t t = blockIdx.x;
-  if (t >= ntiles) return;
-  uint32_t n_deferred = 0;  // wave-uniform
-
-  u32x4 reg[PIECES];
-  SpanTile<VAR> cur = span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, t, lane), lane);
-  span_fetch<PIECES>(reg, cur.base, cur.span16 <= kCap ? cur.span16 : 0u, lane);
-  uint64_t t_next = t + stride;
-  SpanRaw nxt_raw = span_load<VAR>(offsets, n, t_next < ntiles ? t_next : t, lane);
-
-  // Main loop: only tiles whose span fits the LDS window are hashed here, so the
-  // loop body's vector-memory traffic is exactly: PIECES span loads (tile t+1),
-  // two offset loads (tile t+2) and the result stores. Larger tiles are listed
-  // and hashed straight from HBM after the loop.
-  while (true) {
-    const bool staged = cur.span16 <= kCap;
-    if (staged) span_stage<PIECES>(span_lds, reg, cur.span16, lane);
-    else {
-      if (n_deferred < kSpanDefer && lane == 0) deferred[n_deferred] = (uint32_t)(t_next - stride);
-      ++n_deferred;
-    }
+  const SpanTile<VAR> ti =
+      span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, blockIdx.x, lane), lane);
+  if (ti.span16 <= cap) {
+    u32x4 reg[PIECES];
+    span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
+    span_stage<PIECES>(span_lds, reg, ti.span16, lane);
     __syncthreads();
-    const bool more = t_next < ntiles;
-    SpanTile<VAR> nxt{};
-    if (more) nxt = span_finish<VAR>(bytes, off_base, key_len, n, nxt_raw, lane);
-    // offsets of the tile after next go out before the span fetch, so nothing
-    // issued after the fetch is needed before the fetch itself is
-    const uint64_t t_nn = t_next + stride;
-    SpanRaw nn_raw = span_load<VAR>(offsets, n, t_nn < ntiles ? t_nn : t, lane);
-    span_fetch<PIECES>(reg, nxt.base, (more && nxt.span16 <= kCap) ? nxt.span16 : 0u, lane);
-
-    if (staged && cur.valid) {
-      const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + cur.start - cur.base);
-      store_result<OUT>(out, cur.key, hash_lds(span_lds, p, cur.len, seed));
+    if (ti.valid) {
+      const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
+      store_result<OUT>(out, ti.key, hash_lds(span_lds, p, ti.len, seed));
     }
-    __syncthreads();
-    if (!more) break;
-    cur = nxt;
-    nxt_raw = nn_raw;
-    t_next = t_nn;
-  }
-
-  // Tiles too large for the window: per-lane loads straight from HBM.
-  auto hash_direct = [&](uint64_t tt) {
-    const SpanTile<VAR> ti = span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, tt, lane), lane);
-    if (ti.valid) store_result<OUT>(out, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
-  };
-  if (n_deferred <= kSpanDefer) {
-    for (uint32_t i = 0; i < n_deferred; ++i) hash_direct(deferred[i]);
-  } else {  // list overflowed: walk this wave's tiles again
-    for (uint64_t tt = blockIdx.x; tt < ntiles; tt += stride) {
-      const SpanTile<VAR> ti =
-          span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, tt, lane), lane);
-      if (ti.span16 > kCap && ti.valid) store_result<OUT>(out, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
-    }
+  } else if (ti.valid) {
+    store_result<OUT>(out, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
   }
 }
 
@@ -595,31 +547,31 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
   return (unsigned)g;
 }
 
-#ifndef SHFHB_SPAN_GRID_MULT
-#define SHFHB_SPAN_GRID_MULT 1  // grid = this many x the resident workgroups (0: one tile per wave)
-#endif
 template <int OUT, bool VAR, int PIECES>
 static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
-                                uint64_t n, uint32_t seed, void* out, hipStream_t st, int slot) {
+                                uint64_t n, uint32_t seed, void* out, hipStream_t st, uint32_t lds) {
   const uint64_t tiles = (n + 63) / 64;
-  const unsigned res =
-      resident_grid(reinterpret_cast<const void*>(&k_span<OUT, VAR, PIECES>), 64, kSpanAlloc, slot);
-  const unsigned cap = SHFHB_SPAN_GRID_MULT ? res * SHFHB_SPAN_GRID_MULT : 0xffffffffu;
-  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3(grid_for(tiles, 1, cap)), dim3(64), kSpanAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, out);
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;  // 137 G keys per launch
+  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3((unsigned)tiles), dim3(64), lds, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, lds - kSpanPad,
+                     out);
   return hipGetLastError();
 }
 
-// Pieces per lane per tile: enough for a fixed-length tile's span (64 keys +
-// up to 15 bytes of misalignment), the whole window for variable lengths.
+// Fixed lengths: a tile's span is at most 64 * key_len + 15 bytes, so the LDS
+// request (and the fetch) is sized to that; variable lengths use the window.
 template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
                               uint64_t n, uint32_t seed, void* out, hipStream_t st) {
-  const int base_slot = 12 + OUT * 6 + (VAR ? 3 : 0);
-  const uint64_t need = VAR ? kSpanCap : (uint64_t)key_len * 64u + 16u;
-  if (need <= 4096) return launch_span_p<OUT, VAR, 4>(bytes, offsets, off_base, key_len, n, seed, out, st, base_slot);
-  if (need <= 8192) return launch_span_p<OUT, VAR, 8>(bytes, offsets, off_base, key_len, n, seed, out, st, base_slot + 1);
-  return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, key_len, n, seed, out, st, base_slot + 2);
+  if constexpr (VAR) {
+    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, out, st, kSpanAlloc);
+  } else {
+    const uint32_t span = ((uint32_t)key_len * 64u + 15u + 15u) & ~15u;
+    const uint32_t lds = (span + kSpanPad + 255u) & ~255u;
+    // (a PIECES = 8 instantiation spills to scratch under hipcc 7.2: use 4 or 20)
+    if (span <= 4096) return launch_span_p<OUT, VAR, 4>(bytes, offsets, off_base, key_len, n, seed, out, st, lds);
+    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, key_len, n, seed, out, st, lds);
+  }
 }
 
 template <int OUT>

@@ -386,7 +386,7 @@ int shf_hash_batch_fixed_kernel_async(const void* d_keys, uint32_t key_len, uint
   if (n == 0) return SHF_HB_OK;
   if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   if (kernel < SHF_HB_KERNEL_AUTO || kernel > SHF_HB_KERNEL_SPAN) return SHF_HB_ERR_ARG;
-  if (kernel == SHF_HB_KERNEL_SPAN && (uint64_t)key_len * 64u + 16u > 19904u) return SHF_HB_ERR_ARG;
+  if (kernel == SHF_HB_KERNEL_SPAN && (uint64_t)key_len * 64u + 16u > 20416u) return SHF_HB_ERR_ARG;
   if (kernel == SHF_HB_KERNEL_FIXED16 && (key_len != 16 || ((uintptr_t)d_keys & 15u))) return SHF_HB_ERR_ARG;
   if (kernel == SHF_HB_KERNEL_TILED && (key_len < 32 || (key_len & 15u) || ((uintptr_t)d_keys & 15u)))
     return SHF_HB_ERR_ARG;

@@ -41,7 +41,7 @@ def fixed_kernels(key_len, aligned=True):
         ks.append(1)
     if key_len >= 32 and key_len % 16 == 0 and aligned:
         ks.append(2)
-    if key_len * 64 + 16 <= 19904:
+    if key_len * 64 + 16 <= 20416:
         ks.append(4)  # SPAN
     return ks
 
@@ -166,9 +166,9 @@ def test_var_span_edges(hb, dev, oracle):
     cases = [
         np.zeros(200, dtype=np.int64),                                 # every tile empty
         np.concatenate([np.zeros(64, np.int64), rng.integers(0, 40, 100)]),
-        np.full(64, 311, dtype=np.int64),                              # 19904 B: exactly the window
-        np.full(64, 310, dtype=np.int64),
-        np.full(64, 312, dtype=np.int64),                              # just over: deferred tile
+        np.full(64, 319, dtype=np.int64),                              # 20416 B: exactly the window
+        np.full(64, 318, dtype=np.int64),
+        np.full(64, 320, dtype=np.int64),                              # just over: direct from HBM
         np.full(130, 321, dtype=np.int64),                             # > window: fallback tiles
         np.concatenate([np.full(63, 1, np.int64), [20000], np.full(65, 7, np.int64)]),
         rng.integers(300, 340, size=1000),                             # straddles the window size
@@ -187,10 +187,8 @@ def test_var_span_edges(hb, dev, oracle):
             assert np.array_equal(got, want), (lens[:3], k)
 
 
-def test_var_many_tiles_per_workgroup(hb, dev, oracle):
-    """Enough tiles that every workgroup walks many of them (register prefetch
-    of tile t+1 and the offsets of t+2 while t is hashed), with some tiles
-    over the LDS window in between (global fallback)."""
+def test_var_many_tiles(hb, dev, oracle):
+    """A large batch (23k tiles) with a few tiles over the LDS window in between."""
     rng = np.random.default_rng(23)
     n = 1_500_000
     lens = rng.integers(0, 64, size=n)
@@ -208,9 +206,9 @@ def test_var_many_tiles_per_workgroup(hb, dev, oracle):
     assert np.array_equal(got, oracle.hash_fixed(flat, 37))
 
 
-def test_var_deferred_list_overflow(hb, dev, oracle):
-    """More oversized tiles per workgroup than the 128-entry deferred list holds
-    (the kernel then re-walks its tiles), mixed with staged tiles."""
+def test_var_many_oversized_tiles(hb, dev, oracle):
+    """Half of the tiles too large for the LDS window (hashed from HBM), mixed
+    with staged tiles."""
     rng = np.random.default_rng(29)
     n = 64 * 3000 * 4
     lens = rng.integers(0, 40, size=n)
@@ -225,12 +223,11 @@ def test_var_deferred_list_overflow(hb, dev, oracle):
 
 
 def test_var_near_window_and_deferred_mixed(hb, dev, oracle):
-    """Many tiles per workgroup whose spans straddle the LDS window: staged
-    tiles that use the window's last 1 KiB piece interleaved with deferred ones
-    (the staged bytes must never reach the deferred-tile list)."""
+    """Spans straddling the LDS window: staged tiles that use the window's last
+    1 KiB piece (partially) interleaved with tiles hashed from HBM."""
     rng = np.random.default_rng(31)
     n = 64 * 30000
-    lens = rng.integers(300, 322, size=n)
+    lens = rng.integers(308, 330, size=n)
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens)
     data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
