@@ -110,3 +110,23 @@ def test_no_device_fails_loudly_not_on_cpu(hb):
 def test_missing_library_raises(tmp_path):
     with pytest.raises(RuntimeError):
         hbmod.load(str(tmp_path / "nope.so"))
+
+
+def test_kernels_compile_without_scratch():
+    """Every kernel instantiation fits in registers (no scratch spills), as
+    reported by hipcc's resource-usage remarks for gfx950."""
+    import re
+    import shutil
+    import tempfile
+
+    from sharedhashfile_amd import build as b
+
+    if not shutil.which(b.hipcc()) and not os.path.exists(b.hipcc()):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        p = subprocess.run([b.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
+                            os.path.join(b.CSRC, "kernels.hip"), "-o", os.path.join(d, "k.o"),
+                            "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    scratch = [int(x) for x in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", p.stderr)]
+    assert len(scratch) >= 10 and max(scratch) == 0, scratch
