@@ -201,7 +201,7 @@ int drain_slot(DevCtx* c, int s, Pending& p) {
 }
 
 // Host-memory fixed-length pipeline on the current device.
-int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out) {
+int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -233,7 +233,7 @@ int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
 
 // Host-memory variable-length pipeline: chunks of whole keys up to kStageBytes
 // of key bytes (a single larger key gets a chunk of its own).
-int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
+int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -285,6 +285,28 @@ int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t
   for (int s = 0; s < kSlots; ++s)
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
   return SHF_HB_OK;
+}
+
+// On an error mid-pipeline, chunks may still be in flight, some DMA-ing into
+// the caller's (page-locked) output: wait for them before handing the buffers
+// back to the caller.
+int drain_on_error(int rc) {
+  if (rc == SHF_HB_OK) return rc;
+  const int hip = tls_last_hip;
+  DevCtx* c = nullptr;
+  if (current_ctx(&c) == SHF_HB_OK)
+    for (int s = 0; s < kSlots; ++s) (void)hipStreamSynchronize(c->st[s]);
+  (void)hipGetLastError();
+  tls_last_hip = hip;
+  return rc;
+}
+
+int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out) {
+  return drain_on_error(host_fixed_run(keys, key_len, n, seed, out));
+}
+
+int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
+  return drain_on_error(host_var_run(bytes, offsets, n, seed, out));
 }
 
 int check_var_lengths_host(const uint64_t* offsets, uint64_t n) {
