@@ -133,6 +133,76 @@ SHF_HB_API int shf_hash_batch_fixed_kernel_async(const void *d_keys, uint32_t ke
 SHF_HB_API int shf_hash_batch_var_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                     uint32_t seed, shf_hash128 *d_out, int kernel, void *hip_stream);
 
+/* ---- row pre-probe ----------------------------------------
+ *
+ * The first half of shf_find_key_internal() (/root/reference/src/shf.c:886-922)
+ * for a whole batch: hash each key, pick its window, tab and row, and scan the
+ * row's 16 refs for the ones whose pos != 0, rnd and tab match (shf.c:919-921),
+ * against a copy of the store's rows kept in HBM (a "row index"). What is left
+ * for the CPU is the key compare and the value copy at the returned pos.
+ *
+ * The index is a snapshot: rows change under put/del/part/shrink, so a result
+ * is a hint to verify (the key compare does that) and a key with no candidate
+ * goes through the ordinary shf_get_key_val_*() path. INTEGRATION.md §6 shows
+ * the exporter a maintainer adds to shf.c and the resulting get loop.
+ *
+ * Index layout (device memory owned by the shf_row_index handle):
+ *   tab_slot[(win << 11) | tab2] = (slot << 11) | tab, or SHF_PROBE_NONE
+ *       tab  = SHF_WIN_MMAP.tabs[tab2].tab of window win (shf.private.h:85,
+ *              read at shf.c:806 / :906), i.e. which physical tab holds tab2's refs;
+ *       slot = which 64-KiB block of `rows` holds that tab's rows.
+ *       SHF_ROW_INDEX_TABS = 256 * 2048 entries.
+ *   rows[slot] = SHF_TAB_MMAP.row[0..511] of that tab (shf.private.h:59-66),
+ *       byte for byte: 512 rows x 16 refs x 8 B, ref = SHF_REF_MMAP
+ *       {u32 tab:11 | rnd:21 << 11, u32 pos} (shf.private.h:48-52). */
+#define SHF_PROBE_NONE 0xffffffffu        /* = SHF_UID_NONE (shf.h:354) */
+#define SHF_ROW_INDEX_TABS (256u * 2048u) /* tab_slot entries */
+#define SHF_ROW_INDEX_SLOT_BYTES 65536u   /* 512 rows x 128 B */
+
+/* One probe result per key. */
+typedef struct shf_probe {
+    uint32_t uid;  /* SHF_UID.as_u32 (win | tab2 << 8 | row << 19 | ref << 28, shf.private.h:170-178)
+                      of the first candidate ref, or SHF_PROBE_NONE; this is the shf_uid a successful
+                      get returns when the first candidate's key matches */
+    uint32_t pos;  /* that ref's pos: offset of its key,value record in the tab (0 if none) */
+    uint16_t mask; /* bit r set: ref r of the row is a candidate (pos != 0, rnd, tab2 match) */
+    uint16_t tab;  /* physical tab (wins[win].tabs[tab2].tab), 0xffff if the window/tab is not indexed */
+    uint32_t slot; /* rows slot scanned, SHF_PROBE_NONE if none */
+} shf_probe;
+
+typedef struct shf_row_index shf_row_index; /* opaque; lives on the device current at create */
+
+/* Allocate an index of n_slots row blocks on the current device: every
+ * tab_slot entry SHF_PROBE_NONE, every row empty. */
+SHF_HB_API int shf_row_index_create(uint64_t n_slots, shf_row_index **out);
+SHF_HB_API int shf_row_index_destroy(shf_row_index *index);
+/* Copy SHF_ROW_INDEX_TABS entries (host or device memory) into the index
+ * (entries naming a slot >= n_slots are treated as absent by the probes). */
+SHF_HB_API int shf_row_index_set_tabs(shf_row_index *index, const uint32_t *tab_slot);
+/* Copy count row blocks (count * 64 KiB, host or device memory) into slots
+ * [first, first + count). Synchronous. */
+SHF_HB_API int shf_row_index_set_rows(shf_row_index *index, uint64_t first, uint64_t count, const void *rows);
+/* Device pointers of the index, for producers that fill it on the device. */
+SHF_HB_API int shf_row_index_device_ptrs(const shf_row_index *index, uint32_t **d_tab_slot, void **d_rows,
+                                         uint64_t *n_slots);
+
+/* Hash and probe device-resident keys (same key layouts as above). d_hashes
+ * may be NULL; if not, it receives the n SHF_HASH records as well. */
+SHF_HB_API int shf_probe_batch_fixed_async(const shf_row_index *index, const void *d_keys, uint32_t key_len,
+                                           uint64_t n, uint32_t seed, shf_hash128 *d_hashes, shf_probe *d_probe,
+                                           void *hip_stream);
+SHF_HB_API int shf_probe_batch_var_async(const shf_row_index *index, const void *d_bytes,
+                                         const uint64_t *d_offsets, uint64_t n, uint32_t seed,
+                                         shf_hash128 *d_hashes, shf_probe *d_probe, void *hip_stream);
+/* Probe precomputed hashes (n records on the device). */
+SHF_HB_API int shf_probe_batch_hashes_async(const shf_row_index *index, const shf_hash128 *d_hashes, uint64_t n,
+                                            shf_probe *d_probe, void *hip_stream);
+/* Fixed-length probe with a forced hashing kernel (tests and benchmarks). */
+SHF_HB_API int shf_probe_batch_fixed_kernel_async(const shf_row_index *index, const void *d_keys,
+                                                  uint32_t key_len, uint64_t n, uint32_t seed,
+                                                  shf_hash128 *d_hashes, shf_probe *d_probe, int kernel,
+                                                  void *hip_stream);
+
 /* ---- info ----------------------------------------------------------------- */
 SHF_HB_API int shf_hash_batch_device_count(void);          /* visible HIP devices, or a negative status */
 SHF_HB_API int shf_hash_batch_check_device(void);          /* SHF_HB_OK if the current device can run the kernels */

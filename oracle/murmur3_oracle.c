@@ -155,6 +155,58 @@ void oracle_uid_parts_batch(const void *hashes, uint64_t n, uint64_t *parts)
     for (uint64_t i = 0; i < n; ++i) parts[i] = oracle_uid_parts(h + 2 * i);
 }
 
+/* shf_find_key_internal(), SHF_UID_NONE branch (shf.c:886-922), up to the key
+ * compare:
+ *   win  = shf_hash.u16[0] % 256        shf.c:893
+ *   tab2 = shf_hash.u16[1] % 2048       shf.c:894
+ *   row  = shf_hash.u16[2] % 512        shf.c:895
+ *   rnd  = shf_hash.u32[2] % 2^21       shf.c:896
+ *   tab  = wins[win].tabs[tab2].tab     shf.c:906 (the index folds it into tab_slot)
+ *   for ref in 0..15: candidate if pos != 0 && ref.rnd == rnd && ref.tab == tab2  shf.c:918-921
+ * SHF_REF_MMAP (shf.private.h:48-52): a packed u32 bitfield tab:11 then rnd:21
+ * (gcc allocates from bit 0 on x86-64), then u32 pos. The uid of a hit is
+ * SHF_UID with ref = the first candidate (shf.c:931-932, shf.private.h:170-178). */
+void oracle_probe(const void *hashes, uint64_t n, const uint32_t *tab_slot, const void *rows, uint64_t n_slots,
+                  uint32_t *out)
+{
+    const uint64_t *h = (const uint64_t *)hashes;
+    const uint8_t *rb = (const uint8_t *)rows;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t h1 = h[2 * i], h2 = h[2 * i + 1];
+        const uint32_t win = (uint32_t)((h1 & 0xffff) % 256);
+        const uint32_t tab2 = (uint32_t)(((h1 >> 16) & 0xffff) % 2048);
+        const uint32_t row = (uint32_t)(((h1 >> 32) & 0xffff) % 512);
+        const uint32_t rnd = (uint32_t)((h2 & 0xffffffffu) % (1u << 21));
+        uint32_t *o = out + 4 * i;
+        o[0] = 0xffffffffu;
+        o[1] = 0;
+        o[2] = 0xffffu << 16;
+        o[3] = 0xffffffffu;
+        const uint32_t e = tab_slot[(win << 11) | tab2];
+        if (e == 0xffffffffu || (uint64_t)(e >> 11) >= n_slots) continue;
+        const uint32_t slot = e >> 11, tab = e & 0x7ff;
+        const uint8_t *r = rb + (uint64_t)slot * 65536u + (uint64_t)row * 128u;
+        uint32_t mask = 0, first = 16, pos = 0;
+        for (uint32_t ref = 0; ref < 16; ++ref) {
+            uint32_t word, rpos;
+            memcpy(&word, r + 8 * ref, 4);
+            memcpy(&rpos, r + 8 * ref + 4, 4);
+            const uint32_t ref_tab = word & 0x7ff, ref_rnd = word >> 11;
+            if (rpos != 0 && ref_rnd == rnd && ref_tab == tab2) {
+                mask |= 1u << ref;
+                if (first == 16) {
+                    first = ref;
+                    pos = rpos;
+                }
+            }
+        }
+        if (mask) o[0] = win | (tab2 << 8) | (row << 19) | (first << 28);
+        o[1] = pos;
+        o[2] = mask | (tab << 16);
+        o[3] = slot;
+    }
+}
+
 /* SMHasher VerificationTest: hash keys {0}, {0,1}, ... of length i with seed
  * 256 - i, then hash the 256 concatenated 16-byte results with seed 0 and
  * read the first 4 bytes little-endian. */

@@ -30,6 +30,7 @@ class Oracle:
         lib.oracle_hash_fixed_mt.argtypes = [vp, u32, u64, u32, vp, i32]
         lib.oracle_uid_parts_batch.argtypes = [vp, u64, vp]
         lib.oracle_smhasher_verification.restype = u32
+        lib.oracle_probe.argtypes = [vp, u64, vp, vp, u64, vp]
         self.lib = lib
 
     def hash(self, key: bytes, seed=12345):
@@ -66,6 +67,18 @@ class Oracle:
         self.lib.oracle_uid_parts_batch(hashes.ctypes.data, n, out.ctypes.data)
         return out
 
+    def probe(self, hashes, tab_slot, rows, n_slots=None):
+        """Row pre-probe records (n, 4) uint32 {uid, pos, mask | tab << 16, slot}."""
+        hashes = np.ascontiguousarray(hashes, dtype=np.uint64)
+        tab_slot = np.ascontiguousarray(tab_slot, dtype=np.uint32)
+        rows = np.ascontiguousarray(rows).view(np.uint8).reshape(-1)
+        if n_slots is None:
+            n_slots = rows.size // 65536
+        n = hashes.shape[0]
+        out = np.empty((n, 4), dtype=np.uint32)
+        self.lib.oracle_probe(hashes.ctypes.data, n, tab_slot.ctypes.data, rows.ctypes.data, n_slots, out.ctypes.data)
+        return out
+
     def smhasher(self):
         return self.lib.oracle_smhasher_verification()
 
@@ -80,4 +93,32 @@ def reference_lib():
     lib.ref_hash_var.argtypes = [vp, vp, u64, vp]
     lib.ref_bench_make_hash_loop.argtypes = [vp, u32, u64, u64, ctypes.c_int, ctypes.POINTER(u64)]
     lib.ref_bench_make_hash_loop.restype = ctypes.c_double
+    lib.ref_probe_fixture.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, u64, vp, vp, vp, u64]
+    lib.ref_probe_fixture.restype = ctypes.c_int64
     return lib
+
+
+def reference_probe_fixture(data, offsets, n_put, n_query=None, max_slots=4096, folder=None):
+    """Fill a store with the reference's own put (keys [0, n_put)), look up keys
+    [0, n_query) with its own get, export its rows. Returns (uids, tab_slot,
+    rows) as numpy arrays; uids[i] = the reference's shf_uid or 0xffffffff."""
+    import tempfile
+    import uuid
+
+    lib = reference_lib()
+    if lib is None:
+        raise RuntimeError("oracle/_ref/libref_shf.so not built")
+    data = np.ascontiguousarray(data).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if n_query is None:
+        n_query = offsets.size - 1
+    uids = np.empty(n_query, dtype=np.uint32)
+    tab_slot = np.empty(256 * 2048, dtype=np.uint32)
+    rows = np.zeros(max_slots * 65536, dtype=np.uint8)
+    with tempfile.TemporaryDirectory(dir=folder or ("/dev/shm" if os.path.isdir("/dev/shm") else None)) as d:
+        name = "probe" + uuid.uuid4().hex[:8]
+        slots = lib.ref_probe_fixture(d.encode(), name.encode(), data.ctypes.data, offsets.ctypes.data, n_put,
+                                      n_query, uids.ctypes.data, tab_slot.ctypes.data, rows.ctypes.data, max_slots)
+    if slots < 0:
+        raise RuntimeError("ref_probe_fixture failed (%d)" % slots)
+    return uids, tab_slot, rows[: slots * 65536].copy()

@@ -75,6 +75,15 @@ _SIGS = {
     "shf_hash_batch_var_multi": [_VP, _VP, _U64, _U32, _VP, _INT],
     "shf_hash_batch_fixed_kernel_async": [_VP, _U32, _U64, _U32, _VP, _INT, _VP],
     "shf_hash_batch_var_kernel_async": [_VP, _VP, _U64, _U32, _VP, _INT, _VP],
+    "shf_row_index_create": [_U64, ctypes.POINTER(_VP)],
+    "shf_row_index_destroy": [_VP],
+    "shf_row_index_set_tabs": [_VP, _VP],
+    "shf_row_index_set_rows": [_VP, _U64, _U64, _VP],
+    "shf_row_index_device_ptrs": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_U64)],
+    "shf_probe_batch_fixed_async": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _VP],
+    "shf_probe_batch_var_async": [_VP, _VP, _VP, _U64, _U32, _VP, _VP, _VP],
+    "shf_probe_batch_hashes_async": [_VP, _VP, _U64, _VP, _VP],
+    "shf_probe_batch_fixed_kernel_async": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _INT, _VP],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
@@ -204,6 +213,147 @@ def uid_parts_var(data, offsets, seed=SEED, out=None, stream=None):
         ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
         ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_uid_parts_batch_var_async")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Row pre-probe (include/shf_hash_batch.h "row pre-probe")
+# ---------------------------------------------------------------------------
+PROBE_NONE = 0xFFFFFFFF
+ROW_INDEX_TABS = 256 * 2048
+ROW_INDEX_SLOT_BYTES = 65536
+
+
+def _buffer(a, np_dtype):
+    """(pointer, nbytes) of a contiguous numpy array or CUDA tensor, plus the object to keep alive."""
+    try:
+        import torch
+
+        if isinstance(a, torch.Tensor):
+            if not a.is_cuda or not a.is_contiguous():
+                raise ValueError("tensors must be contiguous CUDA tensors")
+            return (ctypes.c_void_p(a.data_ptr()), a.numel() * a.element_size()), a
+    except ImportError:  # pragma: no cover
+        pass
+    arr = np.ascontiguousarray(a)
+    if arr.dtype != np_dtype:
+        arr = arr.view(np_dtype) if arr.dtype.itemsize == np.dtype(np_dtype).itemsize or np_dtype == np.uint8 \
+            else arr.astype(np_dtype)
+    return (ctypes.c_void_p(arr.ctypes.data), arr.nbytes), arr
+
+
+class RowIndex:
+    """Device copy of a store's rows (shf_row_index): tab_slot map + n_slots x 64 KiB.
+
+    tab_slot: (256*2048,) uint32 host array, entry (slot << 11) | tab or PROBE_NONE.
+    rows: (n_slots * 65536,) uint8 host array of SHF_TAB_MMAP.row[] blocks.
+    Either may be omitted and filled later (set_tabs / set_rows / device_ptrs).
+    """
+
+    def __init__(self, n_slots, tab_slot=None, rows=None):
+        lib = load()
+        h = ctypes.c_void_p()
+        _check(lib.shf_row_index_create(int(n_slots), ctypes.byref(h)), "shf_row_index_create")
+        self._h = h
+        self.n_slots = int(n_slots)
+        if tab_slot is not None:
+            self.set_tabs(tab_slot)
+        if rows is not None:
+            self.set_rows(0, rows)
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("row index destroyed")
+        return self._h
+
+    def set_tabs(self, tab_slot):
+        """tab_slot: numpy uint32 array or CUDA tensor (int32/uint32 bits) of 256*2048 entries."""
+        t, keep = _buffer(tab_slot, np.uint32)
+        if t[1] != ROW_INDEX_TABS * 4:
+            raise ValueError("tab_slot needs %d entries" % ROW_INDEX_TABS)
+        _check(load().shf_row_index_set_tabs(self.handle, t[0]), "shf_row_index_set_tabs")
+        del keep
+
+    def set_rows(self, first, rows):
+        """rows: whole 64 KiB slots, numpy array or CUDA tensor."""
+        r, keep = _buffer(rows, np.uint8)
+        if r[1] % ROW_INDEX_SLOT_BYTES:
+            raise ValueError("rows must be whole 64 KiB slots")
+        _check(load().shf_row_index_set_rows(self.handle, int(first), r[1] // ROW_INDEX_SLOT_BYTES, r[0]),
+               "shf_row_index_set_rows")
+        del keep
+
+    def device_ptrs(self):
+        ts, rows, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        _check(load().shf_row_index_device_ptrs(self.handle, ctypes.byref(ts), ctypes.byref(rows), ctypes.byref(n)),
+               "shf_row_index_device_ptrs")
+        return ts.value, rows.value, n.value
+
+    def close(self):
+        if self._h is not None:
+            load().shf_row_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def probe_fixed(index, keys, key_len=None, seed=SEED, out=None, hashes=False, stream=None, kernel=KERNEL_AUTO):
+    """Hash + row pre-probe of fixed-length keys on the GPU.
+
+    Returns an int32 CUDA tensor (n, 4): {uid, pos, mask | tab << 16, slot} per key
+    (struct shf_probe), and with hashes=True also the (n, 2) int64 hash tensor.
+    """
+    import torch
+
+    _require_cuda_u8(keys, "keys")
+    if key_len is None:
+        n, key_len = keys.shape
+    else:
+        n = keys.numel() // key_len if key_len else 0
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=keys.device)
+    hout = torch.empty((n, 2), dtype=torch.int64, device=keys.device) if hashes else None
+    rc = load().shf_probe_batch_fixed_kernel_async(
+        index.handle, ctypes.c_void_p(keys.data_ptr()), key_len, n, seed,
+        ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()), kernel,
+        _stream_handle(stream))
+    _check(rc, "shf_probe_batch_fixed_kernel_async")
+    return (out, hout) if hashes else out
+
+
+def probe_var(index, data, offsets, seed=SEED, out=None, hashes=False, stream=None):
+    import torch
+
+    _require_cuda_u8(data, "data")
+    n = max(offsets.numel() - 1, 0)
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=data.device)
+    hout = torch.empty((n, 2), dtype=torch.int64, device=data.device) if hashes else None
+    rc = load().shf_probe_batch_var_async(
+        index.handle, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
+        ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()),
+        _stream_handle(stream))
+    _check(rc, "shf_probe_batch_var_async")
+    return (out, hout) if hashes else out
+
+
+def probe_hashes(index, hashes, out=None, stream=None):
+    """Row pre-probe of precomputed (n, 2) int64 CUDA hashes."""
+    import torch
+
+    if not (isinstance(hashes, torch.Tensor) and hashes.is_cuda and hashes.is_contiguous()):
+        raise TypeError("hashes must be a contiguous CUDA tensor")
+    n = hashes.shape[0]
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=hashes.device)
+    rc = load().shf_probe_batch_hashes_async(index.handle, ctypes.c_void_p(hashes.data_ptr()), n,
+                                             ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _check(rc, "shf_probe_batch_hashes_async")
     return out
 
 

@@ -6,15 +6,30 @@
 
 namespace shfhb {
 
-enum OutMode { kOutHash = 0, kOutUid = 1 };
+// kOutHash: 16-B SHF_HASH records; kOutUid: 8-B packed UID parts;
+// kOutProbe: 16-B shf_probe records (row pre-probe), plus the
+// hashes when Sink::hash_out is set.
+enum OutMode { kOutHash = 0, kOutUid = 1, kOutProbe = 2 };
 enum KernelChoice { kKernelAuto = 0, kKernelFixed16 = 1, kKernelTiled = 2, kKernelGeneric = 3, kKernelSpan = 4 };
 
-// keys: device pointer to n * key_len bytes; out: n x 16 B (hash) or n x 8 B (uid).
-hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out, int out_mode,
-                        hipStream_t st, int kernel);
+// Where a kernel's per-key result goes (passed by value as a kernel argument).
+struct Sink {
+  void* out = nullptr;                // n records of the OutMode's type
+  void* hash_out = nullptr;           // kOutProbe: optional n x 16-B hashes
+  const uint32_t* tab_slot = nullptr;  // kOutProbe: row index, see shf_hash_batch.h
+  const uint8_t* rows = nullptr;
+  uint64_t n_slots = 0;
+};
+
+// keys: device pointer to n * key_len bytes.
+hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
+                        int out_mode, hipStream_t st, int kernel);
 
 // Key i = bytes[offsets[i] - off_base, offsets[i+1] - off_base); offsets on device.
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
-                      void* out, int out_mode, hipStream_t st, int kernel = kKernelAuto);
+                      const Sink& sink, int out_mode, hipStream_t st, int kernel = kKernelAuto);
+
+// Row pre-probe of precomputed hashes (n x 16 B on device) into sink.out.
+hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st);
 
 }  // namespace shfhb

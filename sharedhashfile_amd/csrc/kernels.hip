@@ -35,14 +35,80 @@ typedef __attribute__((address_space(1))) const u32x4 g_u32x4;          // globa
 typedef __attribute__((address_space(1))) const u32x4_a4 g_u32x4_a4;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
 
+// ---------------------------------------------------------------------------
+// Row pre-probe: the row scan of shf_find_key_internal()
+// (/root/reference/src/shf.c:886-922) against a device copy of the store's rows.
+//   win/tab2/row/rnd from the hash      shf.c:893-896
+//   tab = wins[win].tabs[tab2].tab      shf.c:906   (folded into tab_slot)
+//   candidate ref: pos != 0, rnd == rnd, tab == tab2, first in ref order  shf.c:919-922
+// SHF_REF_MMAP (shf.private.h:48-52) is {u32 tab:11 | rnd:21 << 11, u32 pos}, so
+// a ref matches when its first word equals tab2 | rnd << 11 and pos != 0.
+// Record (shf_probe, shf_hash_batch.h): {uid, pos, mask | tab << 16, slot}.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kProbeNone = 0xffffffffu;  // SHF_UID_NONE (shf.h:354) / no slot
+constexpr uint32_t kRowsPerTabShift = 16;     // 512 rows x 128 B = 64 KiB per slot
+
+__device__ __forceinline__ u32x4 probe_row(const Sink& k, const State& s) {
+  const uint32_t lo = (uint32_t)s.h1;
+  const uint32_t win = lo & 0xffu;
+  const uint32_t tab2 = (lo >> 16) & 0x7ffu;
+  const uint32_t row = (uint32_t)(s.h1 >> 32) & 0x1ffu;
+  const uint32_t rnd = (uint32_t)s.h2 & 0x1fffffu;
+  const uint32_t e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.tab_slot))[(win << 11) | tab2];
+  u32x4 rec = {kProbeNone, 0u, 0xffffu << 16, kProbeNone};
+  if (e != kProbeNone && (uint64_t)(e >> 11) < k.n_slots) {
+    const uint32_t slot = e >> 11;
+    const g_u32x4* r = reinterpret_cast<const g_u32x4*>(reinterpret_cast<uintptr_t>(k.rows) +
+                                                       ((uint64_t)slot << kRowsPerTabShift) + (row << 7));
+    u32x4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = r[q];
+    const uint32_t want = tab2 | (rnd << 11);
+    uint32_t mask = 0, pos = 0, first = 0;
+#pragma unroll
+    for (int q = 7; q >= 0; --q) {  // descending: the lowest matching ref is written last
+      if (v[q].w != 0u && v[q].z == want) {
+        mask |= 2u << (2 * q);
+        pos = v[q].w;
+        first = 2 * q + 1;
+      }
+      if (v[q].y != 0u && v[q].x == want) {
+        mask |= 1u << (2 * q);
+        pos = v[q].y;
+        first = 2 * q;
+      }
+    }
+    rec.x = mask ? (win | (tab2 << 8) | (row << 19) | (first << 28)) : kProbeNone;
+    rec.y = pos;
+    rec.z = mask | ((e & 0x7ffu) << 16);
+    rec.w = slot;
+  }
+  return rec;
+}
+
 template <int OUT>
-__device__ __forceinline__ void store_result(void* __restrict__ out, uint64_t i, const State& s) {
+__device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const State& s) {
   if constexpr (OUT == kOutHash) {
     u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
-    reinterpret_cast<u32x4*>(out)[i] = v;
+    reinterpret_cast<u32x4*>(sink.out)[i] = v;
+  } else if constexpr (OUT == kOutUid) {
+    reinterpret_cast<uint64_t*>(sink.out)[i] = uid_parts(s);
   } else {
-    reinterpret_cast<uint64_t*>(out)[i] = uid_parts(s);
+    if (sink.hash_out) {
+      u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
+      reinterpret_cast<u32x4*>(sink.hash_out)[i] = v;
+    }
+    reinterpret_cast<u32x4*>(sink.out)[i] = probe_row(sink, s);
   }
+}
+
+// Probe precomputed hashes: one lane per key.
+__global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ hashes, uint64_t n, Sink sink) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 h = __builtin_nontemporal_load(&hashes[i]);
+  const State s{pack64(h.x, h.y), pack64(h.z, h.w)};
+  reinterpret_cast<u32x4*>(sink.out)[i] = probe_row(sink, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -56,7 +122,7 @@ __device__ __forceinline__ void store_result(void* __restrict__ out, uint64_t i,
 #endif
 template <int OUT>
 __global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
-                                                 void* __restrict__ out) {
+                                                 Sink sink) {
   constexpr int U = SHFHB_F16_UNROLL;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,7 +136,7 @@ __global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys,
       State s{seed, seed};
       body_block(s, pack64(k[u].x, k[u].y), pack64(k[u].z, k[u].w));
       finish(s, 16);
-      store_result<OUT>(out, i + u * stride, s);
+      store_result<OUT>(sink, i + u * stride, s);
     }
   }
   for (; i < n; i += stride) {
@@ -78,7 +144,7 @@ __global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys,
     State s{seed, seed};
     body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
     finish(s, 16);
-    store_result<OUT>(out, i, s);
+    store_result<OUT>(sink, i, s);
   }
 }
 
@@ -149,7 +215,7 @@ template <int OUT, bool VAR>
 __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ bytes,
                                                  const uint64_t* __restrict__ offsets, uint64_t off_base,
                                                  uint32_t key_len, uint64_t n, uint32_t seed,
-                                                 void* __restrict__ out) {
+                                                 Sink sink) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     uint64_t start;
@@ -163,7 +229,7 @@ __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ byt
       len = key_len;
     }
     const State s = hash_bytes(bytes + start, len, seed);
-    store_result<OUT>(out, i, s);
+    store_result<OUT>(sink, i, s);
   }
 }
 
@@ -205,7 +271,7 @@ __device__ __forceinline__ uint32_t tile_slot(uint32_t key, uint32_t piece) {
 
 template <int OUT, int R>
 __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __restrict__ keys, uint32_t key_len,
-                                                            uint64_t n, uint32_t seed, void* __restrict__ out) {
+                                                            uint64_t n, uint32_t seed, Sink sink) {
   static_assert(R == 4 || R == 8 || R == 16, "pieces per key per round");
   constexpr int kTiledBatch = SHFHB_TILED_BATCH < R ? SHFHB_TILED_BATCH : R;
   constexpr uint32_t kKeysPerInstr = 64 / R;
@@ -301,7 +367,7 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
     if (r + 1 == rounds) {
       const uint64_t key = t * kTileKeys + lane;
       finish(s, key_len);
-      if (key < n) store_result<OUT>(out, key, s);
+      if (key < n) store_result<OUT>(sink, key, s);
       s = State{seed, seed};
     }
     if (!more) break;
@@ -491,7 +557,7 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
 template <int OUT, bool VAR, int PIECES>
 __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
-                                             uint32_t cap, void* __restrict__ out) {
+                                             uint32_t cap, Sink sink) {
   extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
   const uint32_t lane = threadIdx.x;
   const SpanTile<VAR> ti =
@@ -503,10 +569,10 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
     __syncthreads();
     if (ti.valid) {
       const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-      store_result<OUT>(out, ti.key, hash_lds(span_lds, p, ti.len, seed));
+      store_result<OUT>(sink, ti.key, hash_lds(span_lds, p, ti.len, seed));
     }
   } else if (ti.valid) {
-    store_result<OUT>(out, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
+    store_result<OUT>(sink, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
   }
 }
 
@@ -529,15 +595,19 @@ static unsigned resident_grid(const void* kernel, int block, size_t dyn_lds, int
   return g;
 }
 
-// Pieces (16 B) of every key staged per round by k_tiled: 8 (one 128-B line per
-// key) unless SHF_HB_TILED_ROUND=4|16 overrides it (a tuning knob, read once).
-static int tiled_round_pieces() {
-  static const int r = [] {
+// Pieces (16 B) of every key staged per round by k_tiled. 8 (one 128-B line per
+// key per round) when every round is full; otherwise 16, so that a key of
+// 12-15 pieces is one round instead of a full and a mostly empty one
+// (profiles/r1/sweep_tiled: L=192 5167 GB/s at 16 vs 3689 at 8).
+// SHF_HB_TILED_ROUND=4|8|16 overrides it (a tuning knob, read once).
+static int tiled_round_pieces(uint32_t key_len) {
+  static const int forced = [] {
     const char* e = getenv("SHF_HB_TILED_ROUND");
-    const int v = e ? atoi(e) : 8;
-    return (v == 4 || v == 16) ? v : 8;
+    const int v = e ? atoi(e) : 0;
+    return (v == 4 || v == 8 || v == 16) ? v : 0;
   }();
-  return r;
+  if (forced) return forced;
+  return ((key_len >> 4) & 7u) == 0 ? 8 : 16;
 }
 
 static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
@@ -549,12 +619,12 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
 
 template <int OUT, bool VAR, int PIECES>
 static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
-                                uint64_t n, uint32_t seed, void* out, hipStream_t st, uint32_t lds) {
+                                uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint32_t lds) {
   const uint64_t tiles = (n + 63) / 64;
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;  // 137 G keys per launch
   hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3((unsigned)tiles), dim3(64), lds, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, lds - kSpanPad,
-                     out);
+                     sink);
   return hipGetLastError();
 }
 
@@ -562,44 +632,51 @@ static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint
 // request (and the fetch) is sized to that; variable lengths use the window.
 template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
-                              uint64_t n, uint32_t seed, void* out, hipStream_t st) {
+                              uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st) {
   if constexpr (VAR) {
-    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, out, st, kSpanAlloc);
+    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, kSpanAlloc);
   } else {
     const uint32_t span = ((uint32_t)key_len * 64u + 15u + 15u) & ~15u;
     const uint32_t lds = (span + kSpanPad + 255u) & ~255u;
     // (a PIECES = 8 instantiation spills to scratch under hipcc 7.2: use 4 or 20)
-    if (span <= 4096) return launch_span_p<OUT, VAR, 4>(bytes, offsets, off_base, key_len, n, seed, out, st, lds);
-    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, key_len, n, seed, out, st, lds);
+    if (span <= 4096) return launch_span_p<OUT, VAR, 4>(bytes, offsets, off_base, key_len, n, seed, sink, st, lds);
+    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, key_len, n, seed, sink, st, lds);
   }
 }
 
 template <int OUT>
-static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out,
+static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
                                  hipStream_t st, int kernel) {
   const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
   if (kernel == kKernelAuto) {
-    // Measured on MI355X, 6.4 GB batches (tools/sweep_fixed.sh, profiles/r1):
-    //  - k_tiled wins when every round is full (key_len a multiple of 128 B);
-    //  - k_span wins for lengths whose 64-key tiles fit its LDS window, except
-    //    multiples of 64 B, whose lane-per-key LDS reads all hit the same banks;
+    // Measured on MI355X, 6.4 GB batches (tools/sweep_fixed.sh, tools/sweep_tiled*.sh,
+    // profiles/r1/sweep_fixed_v2, profiles/r1/sweep_tiled):
+    //  - k_tiled (8 pieces per round) when every round is full: key_len % 128 == 0;
+    //  - k_span for lengths whose 64-key tiles fit its LDS window, except
+    //    multiples of 64 B, whose lane-per-key LDS reads all hit the same banks
+    //    (L=144..240: 5191-5680 GB/s against 4871-5423 for k_tiled<16>);
+    //  - k_tiled (16 pieces per round) when its one partial round is >= 3/4 full
+    //    (L=192: 5167 against generic 4564, span 4197);
     //  - short keys (< 48 B) and the rest: per-lane loads (k_generic).
+    const uint32_t pieces = key_len >> 4;
+    const bool whole16 = (key_len & 15u) == 0 && al16;
     if (key_len == 16 && al16) kernel = kKernelFixed16;
-    else if (key_len >= 128 && (key_len & 127u) == 0 && al16) kernel = kKernelTiled;
+    else if (whole16 && key_len >= 128 && (pieces & 7u) == 0) kernel = kKernelTiled;
     else if (key_len >= 48 && (key_len & 63u) != 0 && (uint64_t)key_len * 64u + 16u <= kSpanCap)
       kernel = kKernelSpan;
+    else if (whole16 && key_len >= 128 && (pieces & 15u) >= 12) kernel = kKernelTiled;
     else kernel = kKernelGeneric;
   }
   switch (kernel) {
     case kKernelFixed16:
       if (key_len != 16 || !al16) return hipErrorInvalidValue;
       hipLaunchKernelGGL(k_fixed16<OUT>, dim3(grid_for(n, 256, SHFHB_F16_GRID_CAP)), dim3(256), 0, st,
-                         reinterpret_cast<const u32x4*>(keys), n, seed, out);
+                         reinterpret_cast<const u32x4*>(keys), n, seed, sink);
       break;
     case kKernelTiled: {
       if (key_len < 32 || (key_len & 15u) || !al16) return hipErrorInvalidValue;
       const uint64_t tiles = (n + kTileKeys - 1) / kTileKeys;
-      const int r = tiled_round_pieces();
+      const int r = tiled_round_pieces(key_len);
       const void* fn = r == 4    ? reinterpret_cast<const void*>(&k_tiled<OUT, 4>)
                        : r == 16 ? reinterpret_cast<const void*>(&k_tiled<OUT, 16>)
                                  : reinterpret_cast<const void*>(&k_tiled<OUT, 8>);
@@ -607,17 +684,17 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
       const dim3 g(grid_for(tiles, kTiledWaves, SHFHB_TILED_GRID_MULT ? res * SHFHB_TILED_GRID_MULT : 0xffffffffu)),
           b(64 * kTiledWaves);
       const uint8_t* k8 = reinterpret_cast<const uint8_t*>(keys);
-      if (r == 4) hipLaunchKernelGGL((k_tiled<OUT, 4>), g, b, 0, st, k8, key_len, n, seed, out);
-      else if (r == 16) hipLaunchKernelGGL((k_tiled<OUT, 16>), g, b, 0, st, k8, key_len, n, seed, out);
-      else hipLaunchKernelGGL((k_tiled<OUT, 8>), g, b, 0, st, k8, key_len, n, seed, out);
+      if (r == 4) hipLaunchKernelGGL((k_tiled<OUT, 4>), g, b, 0, st, k8, key_len, n, seed, sink);
+      else if (r == 16) hipLaunchKernelGGL((k_tiled<OUT, 16>), g, b, 0, st, k8, key_len, n, seed, sink);
+      else hipLaunchKernelGGL((k_tiled<OUT, 8>), g, b, 0, st, k8, key_len, n, seed, sink);
       break;
     }
     case kKernelSpan:
-      return launch_span<OUT, false>(keys, nullptr, 0, key_len, n, seed, out, st);
+      return launch_span<OUT, false>(keys, nullptr, 0, key_len, n, seed, sink, st);
     default:
       hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                          reinterpret_cast<const uint8_t*>(keys), (const uint64_t*)nullptr, (uint64_t)0, key_len, n,
-                         seed, out);
+                         seed, sink);
       break;
   }
   return hipGetLastError();
@@ -625,27 +702,47 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
 
 template <int OUT>
 static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                               uint32_t seed, void* out, hipStream_t st, int kernel) {
+                               uint32_t seed, const Sink& sink, hipStream_t st, int kernel) {
   if (kernel == kKernelGeneric) {
     hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, out);
+                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, sink);
     return hipGetLastError();
   }
-  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, out, st);
+  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st);
 }
 
-hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out, int out_mode,
-                        hipStream_t st, int kernel) {
+hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
+                        int out_mode, hipStream_t st, int kernel) {
   if (n == 0) return hipSuccess;
-  return out_mode == kOutHash ? launch_fixed_t<kOutHash>(keys, key_len, n, seed, out, st, kernel)
-                              : launch_fixed_t<kOutUid>(keys, key_len, n, seed, out, st, kernel);
+  switch (out_mode) {
+    case kOutHash:
+      return launch_fixed_t<kOutHash>(keys, key_len, n, seed, sink, st, kernel);
+    case kOutUid:
+      return launch_fixed_t<kOutUid>(keys, key_len, n, seed, sink, st, kernel);
+    default:
+      return launch_fixed_t<kOutProbe>(keys, key_len, n, seed, sink, st, kernel);
+  }
 }
 
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
-                      void* out, int out_mode, hipStream_t st, int kernel) {
+                      const Sink& sink, int out_mode, hipStream_t st, int kernel) {
   if (n == 0) return hipSuccess;
-  return out_mode == kOutHash ? launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, out, st, kernel)
-                              : launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, out, st, kernel);
+  switch (out_mode) {
+    case kOutHash:
+      return launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, sink, st, kernel);
+    case kOutUid:
+      return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel);
+    default:
+      return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel);
+  }
+}
+
+hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if ((n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_probe_hashes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const u32x4*>(hashes), n, sink);
+  return hipGetLastError();
 }
 
 }  // namespace shfhb

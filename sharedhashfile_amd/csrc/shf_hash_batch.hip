@@ -49,6 +49,12 @@ constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `con
 constexpr size_t kStageBytes = (size_t)64 << 20;   // key bytes per pipeline chunk
 constexpr int kSlots = 2;                          // double buffering
 
+shfhb::Sink out_sink(void* out) {
+  shfhb::Sink k;
+  k.out = out;
+  return k;
+}
+
 // Per (thread, device) resources. Created lazily, reused across calls.
 struct DevCtx {
   int dev = -1;
@@ -219,7 +225,7 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     const uint8_t* src = in_pinned ? keys + i0 * key_len : c->h_in[s];
     if (nb && !in_pinned) par_memcpy(c->h_in[s], keys + i0 * key_len, nb);
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], src, nb, hipMemcpyHostToDevice, c->st[s]));
-    HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, c->d_out[s], shfhb::kOutHash, c->st[s],
+    HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, out_sink(c->d_out[s]), shfhb::kOutHash, c->st[s],
                                shfhb::kKernelAuto));
     HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
                           hipMemcpyDeviceToHost, c->st[s]));
@@ -275,7 +281,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], in_pinned ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
                                   c->st[s]));
     HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
-    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, c->d_out[s], shfhb::kOutHash, c->st[s]));
+    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, out_sink(c->d_out[s]), shfhb::kOutHash, c->st[s]));
     HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
                           hipMemcpyDeviceToHost, c->st[s]));
     HB_TRY(hipEventRecord(c->done[s], c->st[s]));
@@ -316,25 +322,68 @@ int check_var_lengths_host(const uint64_t* offsets, uint64_t n) {
   return SHF_HB_OK;
 }
 
-int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, void* out, int out_mode,
-                 hipStream_t st, int kernel, bool sync) {
+int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const shfhb::Sink& sink,
+                 int out_mode, hipStream_t st, int kernel, bool sync) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
   if (sync) st = c->st[0];
-  HB_TRY(shfhb::launch_fixed(keys, key_len, n, seed, out, out_mode, st, kernel));
+  HB_TRY(shfhb::launch_fixed(keys, key_len, n, seed, sink, out_mode, st, kernel));
   if (sync) HB_TRY(hipStreamSynchronize(st));
   return SHF_HB_OK;
 }
 
-int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, void* out, int out_mode,
-               hipStream_t st, bool sync, int kernel = shfhb::kKernelAuto) {
+int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const shfhb::Sink& sink,
+               int out_mode, hipStream_t st, bool sync, int kernel = shfhb::kKernelAuto) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
   if (sync) st = c->st[0];
-  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, out, out_mode, st, kernel));
+  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, sink, out_mode, st, kernel));
   if (sync) HB_TRY(hipStreamSynchronize(st));
+  return SHF_HB_OK;
+}
+
+// Can the forced fixed-length kernel take this shape? (AUTO always can.)
+bool fixed_kernel_fits(const void* d_keys, uint32_t key_len, int kernel) {
+  const bool al16 = ((uintptr_t)d_keys & 15u) == 0;
+  switch (kernel) {
+    case SHF_HB_KERNEL_AUTO:
+    case SHF_HB_KERNEL_GENERIC:
+      return true;
+    case SHF_HB_KERNEL_FIXED16:
+      return key_len == 16 && al16;
+    case SHF_HB_KERNEL_TILED:
+      return key_len >= 32 && (key_len & 15u) == 0 && al16;
+    case SHF_HB_KERNEL_SPAN:
+      return (uint64_t)key_len * 64u + 16u <= 20416u;  // one 64-key tile in the LDS window
+    default:
+      return false;
+  }
+}
+
+// Row index: device copies of a store's tab map and rows (shf_hash_batch.h).
+}  // namespace
+
+struct shf_row_index {
+  int dev = -1;
+  uint32_t* d_tab_slot = nullptr;
+  uint8_t* d_rows = nullptr;
+  uint64_t n_slots = 0;
+};
+
+namespace {
+
+// Probe sink for `index` on the calling thread's current device.
+int probe_sink(const shf_row_index* index, void* d_probe, void* d_hashes, shfhb::Sink* sink) {
+  if (!index || !d_probe) return SHF_HB_ERR_ARG;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != index->dev) return SHF_HB_ERR_ARG;
+  sink->out = d_probe;
+  sink->hash_out = d_hashes;
+  sink->tab_slot = index->d_tab_slot;
+  sink->rows = index->d_rows;
+  sink->n_slots = index->n_slots;
   return SHF_HB_OK;
 }
 
@@ -390,7 +439,7 @@ int shf_hash_batch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_
   if (n == 0) return SHF_HB_OK;
   if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   if (mem == SHF_HASH_MEM_DEVICE)
-    return device_fixed(keys, key_len, n, seed, out, shfhb::kOutHash, nullptr, shfhb::kKernelAuto, true);
+    return device_fixed(keys, key_len, n, seed, out_sink(out), shfhb::kOutHash, nullptr, shfhb::kKernelAuto, true);
   if (mem == SHF_HASH_MEM_HOST) return host_fixed((const uint8_t*)keys, key_len, n, seed, out);
   return SHF_HB_ERR_ARG;
 }
@@ -399,7 +448,7 @@ int shf_hash_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n,
                                void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
-  return device_fixed(d_keys, key_len, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream,
+  return device_fixed(d_keys, key_len, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream,
                       shfhb::kKernelAuto, false);
 }
 
@@ -407,19 +456,15 @@ int shf_hash_batch_fixed_kernel_async(const void* d_keys, uint32_t key_len, uint
                                       shf_hash128* d_out, int kernel, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
-  if (kernel < SHF_HB_KERNEL_AUTO || kernel > SHF_HB_KERNEL_SPAN) return SHF_HB_ERR_ARG;
-  if (kernel == SHF_HB_KERNEL_SPAN && (uint64_t)key_len * 64u + 16u > 20416u) return SHF_HB_ERR_ARG;
-  if (kernel == SHF_HB_KERNEL_FIXED16 && (key_len != 16 || ((uintptr_t)d_keys & 15u))) return SHF_HB_ERR_ARG;
-  if (kernel == SHF_HB_KERNEL_TILED && (key_len < 32 || (key_len & 15u) || ((uintptr_t)d_keys & 15u)))
-    return SHF_HB_ERR_ARG;
-  return device_fixed(d_keys, key_len, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, kernel, false);
+  if (!fixed_kernel_fits(d_keys, key_len, kernel)) return SHF_HB_ERR_ARG;
+  return device_fixed(d_keys, key_len, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, kernel, false);
 }
 
 int shf_hash_batch_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out,
                        int mem) {
   if (n == 0) return SHF_HB_OK;
   if (!out || !offsets || !bytes) return SHF_HB_ERR_ARG;
-  if (mem == SHF_HASH_MEM_DEVICE) return device_var(bytes, offsets, n, seed, out, shfhb::kOutHash, nullptr, true);
+  if (mem == SHF_HASH_MEM_DEVICE) return device_var(bytes, offsets, n, seed, out_sink(out), shfhb::kOutHash, nullptr, true);
   if (mem == SHF_HASH_MEM_HOST) {
     int rc = check_var_lengths_host(offsets, n);
     if (rc) return rc;
@@ -432,7 +477,7 @@ int shf_hash_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uin
                              shf_hash128* d_out, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
-  return device_var(d_bytes, d_offsets, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, false);
+  return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false);
 }
 
 int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
@@ -441,14 +486,14 @@ int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offse
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC)
     return SHF_HB_ERR_ARG;
-  return device_var(d_bytes, d_offsets, n, seed, d_out, shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
+  return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
 }
 
 int shf_uid_parts_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                     uint64_t* d_parts, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_parts || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
-  return device_fixed(d_keys, key_len, n, seed, d_parts, shfhb::kOutUid, (hipStream_t)hip_stream,
+  return device_fixed(d_keys, key_len, n, seed, out_sink(d_parts), shfhb::kOutUid, (hipStream_t)hip_stream,
                       shfhb::kKernelAuto, false);
 }
 
@@ -456,7 +501,7 @@ int shf_uid_parts_batch_var_async(const void* d_bytes, const uint64_t* d_offsets
                                   uint64_t* d_parts, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_parts || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
-  return device_var(d_bytes, d_offsets, n, seed, d_parts, shfhb::kOutUid, (hipStream_t)hip_stream, false);
+  return device_var(d_bytes, d_offsets, n, seed, out_sink(d_parts), shfhb::kOutUid, (hipStream_t)hip_stream, false);
 }
 
 int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
@@ -479,6 +524,104 @@ int shf_hash_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_
   return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
     return host_var(b, offsets + lo, hi - lo, seed, out + lo);
   });
+}
+
+int shf_row_index_create(uint64_t n_slots, shf_row_index** out) {
+  if (!out) return SHF_HB_ERR_ARG;
+  *out = nullptr;
+  if (n_slots > ((uint64_t)1 << 21)) return SHF_HB_ERR_ARG;  // slot must fit the 21 high bits of tab_slot
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  shf_row_index* x = new shf_row_index();
+  x->dev = c->dev;
+  x->n_slots = n_slots;
+  hipError_t e = hipMalloc((void**)&x->d_tab_slot, SHF_ROW_INDEX_TABS * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(x->d_tab_slot, 0xff, SHF_ROW_INDEX_TABS * sizeof(uint32_t));
+  if (e == hipSuccess && n_slots) e = hipMalloc((void**)&x->d_rows, n_slots * SHF_ROW_INDEX_SLOT_BYTES);
+  if (e == hipSuccess && n_slots) e = hipMemset(x->d_rows, 0, n_slots * SHF_ROW_INDEX_SLOT_BYTES);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    (void)shf_row_index_destroy(x);
+    return map_hip(e);
+  }
+  *out = x;
+  return SHF_HB_OK;
+}
+
+int shf_row_index_destroy(shf_row_index* index) {
+  if (!index) return SHF_HB_OK;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(index->dev);
+  if (index->d_tab_slot) (void)hipFree(index->d_tab_slot);
+  if (index->d_rows) (void)hipFree(index->d_rows);
+  (void)hipSetDevice(prev);
+  delete index;
+  return SHF_HB_OK;
+}
+
+int shf_row_index_set_tabs(shf_row_index* index, const uint32_t* tab_slot) {
+  if (!index || !tab_slot) return SHF_HB_ERR_ARG;
+  HB_TRY(hipMemcpy(index->d_tab_slot, tab_slot, SHF_ROW_INDEX_TABS * sizeof(uint32_t), hipMemcpyDefault));
+  return SHF_HB_OK;
+}
+
+int shf_row_index_set_rows(shf_row_index* index, uint64_t first, uint64_t count, const void* rows) {
+  if (!index || (!rows && count) || first > index->n_slots || count > index->n_slots - first) return SHF_HB_ERR_ARG;
+  if (!count) return SHF_HB_OK;
+  HB_TRY(hipMemcpy(index->d_rows + first * SHF_ROW_INDEX_SLOT_BYTES, rows, count * SHF_ROW_INDEX_SLOT_BYTES,
+                   hipMemcpyDefault));
+  return SHF_HB_OK;
+}
+
+int shf_row_index_device_ptrs(const shf_row_index* index, uint32_t** d_tab_slot, void** d_rows, uint64_t* n_slots) {
+  if (!index) return SHF_HB_ERR_ARG;
+  if (d_tab_slot) *d_tab_slot = index->d_tab_slot;
+  if (d_rows) *d_rows = index->d_rows;
+  if (n_slots) *n_slots = index->n_slots;
+  return SHF_HB_OK;
+}
+
+int shf_probe_batch_fixed_kernel_async(const shf_row_index* index, const void* d_keys, uint32_t key_len, uint64_t n,
+                                       uint32_t seed, shf_hash128* d_hashes, shf_probe* d_probe, int kernel,
+                                       void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if ((!d_keys && key_len) || key_len > kMaxKeyLen || !fixed_kernel_fits(d_keys, key_len, kernel))
+    return SHF_HB_ERR_ARG;
+  shfhb::Sink sink;
+  int rc = probe_sink(index, d_probe, d_hashes, &sink);
+  if (rc) return rc;
+  return device_fixed(d_keys, key_len, n, seed, sink, shfhb::kOutProbe, (hipStream_t)hip_stream, kernel, false);
+}
+
+int shf_probe_batch_fixed_async(const shf_row_index* index, const void* d_keys, uint32_t key_len, uint64_t n,
+                                uint32_t seed, shf_hash128* d_hashes, shf_probe* d_probe, void* hip_stream) {
+  return shf_probe_batch_fixed_kernel_async(index, d_keys, key_len, n, seed, d_hashes, d_probe, SHF_HB_KERNEL_AUTO,
+                                            hip_stream);
+}
+
+int shf_probe_batch_var_async(const shf_row_index* index, const void* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                              uint32_t seed, shf_hash128* d_hashes, shf_probe* d_probe, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
+  shfhb::Sink sink;
+  int rc = probe_sink(index, d_probe, d_hashes, &sink);
+  if (rc) return rc;
+  return device_var(d_bytes, d_offsets, n, seed, sink, shfhb::kOutProbe, (hipStream_t)hip_stream, false);
+}
+
+int shf_probe_batch_hashes_async(const shf_row_index* index, const shf_hash128* d_hashes, uint64_t n,
+                                 shf_probe* d_probe, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_hashes) return SHF_HB_ERR_ARG;
+  shfhb::Sink sink;
+  int rc = probe_sink(index, d_probe, nullptr, &sink);
+  if (rc) return rc;
+  DevCtx* c = nullptr;
+  if ((rc = current_ctx(&c))) return rc;
+  HB_TRY(shfhb::launch_probe_hashes(d_hashes, n, sink, (hipStream_t)hip_stream));
+  return SHF_HB_OK;
 }
 
 int shf_hash_batch_device_count(void) { return visible_devices(); }

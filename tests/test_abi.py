@@ -90,6 +90,19 @@ def test_argument_validation_needs_no_device(hb):
                                                  hbmod.KERNEL_TILED, None) == hbmod.ERR_ARG
     assert lib.shf_hash_batch_fixed_kernel_async(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 9,
                                                  None) == hbmod.ERR_ARG
+    # row pre-probe: no index / no output / bad handles
+    assert lib.shf_probe_batch_fixed_async(None, keys.ctypes.data, 16, 4, 12345, None, out.ctypes.data,
+                                           None) == hbmod.ERR_ARG
+    assert lib.shf_probe_batch_var_async(None, keys.ctypes.data, keys.ctypes.data, 2, 12345, None,
+                                         out.ctypes.data, None) == hbmod.ERR_ARG
+    assert lib.shf_probe_batch_hashes_async(None, out.ctypes.data, 4, out.ctypes.data, None) == hbmod.ERR_ARG
+    assert lib.shf_probe_batch_hashes_async(None, None, 0, None, None) == hbmod.OK
+    assert lib.shf_row_index_create(0, None) == hbmod.ERR_ARG
+    assert lib.shf_row_index_create(1 << 22, ctypes.byref(ctypes.c_void_p())) == hbmod.ERR_ARG
+    assert lib.shf_row_index_destroy(None) == hbmod.OK
+    assert lib.shf_row_index_set_tabs(None, keys.ctypes.data) == hbmod.ERR_ARG
+    assert lib.shf_row_index_set_rows(None, 0, 1, keys.ctypes.data) == hbmod.ERR_ARG
+    assert lib.shf_row_index_device_ptrs(None, None, None, None) == hbmod.ERR_ARG
 
 
 @pytest.mark.skipif(_has_gpu(), reason="checks the no-device behaviour")
@@ -105,6 +118,11 @@ def test_no_device_fails_loudly_not_on_cpu(hb):
         hbmod.hash_fixed_host(keys.reshape(4, 16))
     assert lib.shf_hash_batch_fixed_multi(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 0) in (
         hbmod.ERR_NODEV, hbmod.ERR_HIP)
+    h = ctypes.c_void_p()
+    assert lib.shf_row_index_create(4, ctypes.byref(h)) in (hbmod.ERR_NODEV, hbmod.ERR_HIP)
+    assert h.value is None
+    with pytest.raises(hbmod.ShfHashBatchError):
+        hbmod.RowIndex(4)
 
 
 def test_missing_library_raises(tmp_path):
