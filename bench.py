@@ -11,7 +11,9 @@ never inside the timed region).
 Headline (`value`): BASELINE.json configs[1] = 10M fixed 16-byte keys per GPU,
 MurmurHash3_x64_128 seed 12345 (= shf_make_hash, /root/reference/src/shf.c:456)
 -> 16-byte SHF_HASH per key. Also reported (`secondary`): configs[2] (100M x
-256-byte keys) and configs[3] (100M variable-length keys, 8..512 B).
+256-byte keys) and configs[3] (100M variable-length keys, 8..512 B), and the
+row pre-probe: the configs[1] keys hashed and probed against
+a device row index holding all of them (`probe16`).
 
 Multi-GPU: one process per GPU, each hashes its own independent shard (weak
 scaling); torch.distributed (RCCL) is used only for the start/stop barriers and
@@ -50,7 +52,8 @@ def parse():
     p.add_argument("--keys16", type=int, default=10_000_000, help="configs[1]: 16-B keys per GPU")
     p.add_argument("--keys256", type=int, default=100_000_000, help="configs[2]: 256-B keys per GPU")
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
-    p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var (default: all)")
+    p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var,probe16 (default: all)")
+    p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
     p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -94,7 +97,7 @@ def make_workloads(args, dev, rank):
     import sharedhashfile_amd as hb
     from sharedhashfile_amd.keygen import device_random_bytes
 
-    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed256", "var"}
+    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed256", "var", "probe16"}
     wl = []
     seed_base = 0x5348460000000001 + 1000 * rank
     if "fixed16" in only:
@@ -128,6 +131,24 @@ def make_workloads(args, dev, rank):
                            lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3}[args.var_kernel]:
                            hb.hash_var(d, o, out=out, kernel=vk),
                            "k_span" if args.var_kernel != "generic" else "k_generic", "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
+    if "probe16" in only:
+        # Row pre-probe: hash + row scan of every key against an index holding
+        # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +
+        # 16 record; the 2 MiB tab map is read once per launch.
+        from sharedhashfile_amd.rowindex import synthetic_index
+
+        n = args.keys16
+        keys = device_random_bytes(n * 16, seed_base + 5, dev)
+        h = hb.hash_fixed(keys, 16)
+        tab_slot, rows, n_slots, placed = synthetic_index(h, tabs_per_win=args.probe_tabs)
+        index = hb.RowIndex(n_slots, tab_slot, rows)
+        del h, tab_slot, rows
+        out = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        wl.append(Workload("probe16", n, 16 + 128 + 16 + 4 * 256 * 2048 / n,
+                           lambda k=keys, o=out, ix=index: hb.probe_fixed(ix, k, 16, out=o),
+                           "k_fixed16<kOutProbe>", "%d fixed 16-B keys hashed and probed against a row index of "
+                           "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed)))
+        wl[-1].index = index
     torch.cuda.synchronize()
     return wl
 

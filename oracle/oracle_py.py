@@ -95,6 +95,18 @@ def reference_lib():
     lib.ref_bench_make_hash_loop.restype = ctypes.c_double
     lib.ref_probe_fixture.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, u64, vp, vp, vp, u64]
     lib.ref_probe_fixture.restype = ctypes.c_int64
+    lib.ref_export_rows.argtypes = [vp, vp, vp, u64]
+    lib.ref_export_rows.restype = ctypes.c_int64
+    lib.ref_store_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.ref_store_open.restype = vp
+    lib.ref_store_put.argtypes = [vp, vp, vp, u64]
+    lib.ref_store_put.restype = ctypes.c_int64
+    lib.ref_store_close.argtypes = [vp]
+    lib.ref_store_close.restype = None
+    lib.ref_store_get_plain.argtypes = [vp, vp, vp, u64, ctypes.POINTER(ctypes.c_double)]
+    lib.ref_store_get_plain.restype = ctypes.c_int64
+    lib.ref_store_get_probed.argtypes = [vp, vp, vp, u64, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)]
+    lib.ref_store_get_probed.restype = ctypes.c_int64
     return lib
 
 

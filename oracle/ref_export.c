@@ -29,6 +29,7 @@
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <sys/types.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "shf.private.h"
@@ -96,4 +97,88 @@ int64_t ref_probe_fixture(const char *folder, const char *name, const uint8_t *b
     const int64_t slots = ref_export_rows(shf, tab_slot, rows, max_slots);
     (void)shf_del(shf);
     return slots;
+}
+
+/* ---- the f3 get loop, end to end, on the reference's own store ------------
+ * A store that stays open across calls, so a test can export its rows, probe
+ * them on the GPU, and feed the probe records back into the reference's get.
+ * Values are the key index (8 bytes). */
+SHF *ref_store_open(const char *folder, const char *name)
+{
+    shf_init();
+    SHF *shf = shf_attach(folder, name, 0);
+    if (shf) shf_set_is_lockable(shf, 0);
+    return shf;
+}
+
+int64_t ref_store_put(SHF *shf, const uint8_t *bytes, const uint64_t *offsets, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        shf_make_hash((const char *)bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]));
+        if (shf_put_key_val(shf, (const char *)&i, sizeof(i)) != SHF_RET_KEY_PUT) return (int64_t)i;
+    }
+    return (int64_t)n;
+}
+
+void ref_store_close(SHF *shf) { (void)shf_del(shf); }
+
+static double ref_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int ref_val_is(uint64_t i) { return shf_val_len == sizeof(i) && memcmp(shf_val, &i, sizeof(i)) == 0; }
+
+/* The reference's own get loop (test.9.shf.c:442-445 shape): shf_make_hash()
+ * + shf_get_key_val_copy() per key. Returns keys found with the right value. */
+int64_t ref_store_get_plain(SHF *shf, const uint8_t *bytes, const uint64_t *offsets, uint64_t n, double *seconds)
+{
+    int64_t good = 0;
+    const double t0 = ref_now();
+    for (uint64_t i = 0; i < n; ++i) {
+        shf_make_hash((const char *)bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]));
+        good += shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND && ref_val_is(i);
+    }
+    if (seconds) *seconds = ref_now() - t0;
+    return good;
+}
+
+/* The get loop INTEGRATION.md §6 describes, driven by GPU probe records
+ * (4 u32 per key: uid, pos, mask | tab << 16, slot) and GPU hashes:
+ *   candidate -> shf_get_uid_val_copy(uid) (shf.c:1037; checks pos and tab,
+ *                not the key) + compare the stored key (len at key - 4,
+ *                then the bytes) -> done;
+ *   otherwise  -> the ordinary get with the GPU hash in the thread-local
+ *                seam (test.9.shf.c:176-182).
+ * Returns keys found with the right value; *fast = keys served by the uid path. */
+int64_t ref_store_get_probed(SHF *shf, const uint8_t *bytes, const uint64_t *offsets, uint64_t n,
+                             const uint32_t *probe, const uint64_t *hashes, uint64_t *fast, double *seconds)
+{
+    int64_t good = 0;
+    uint64_t f = 0;
+    const double t0 = ref_now();
+    for (uint64_t i = 0; i < n; ++i) {
+        const char *k = (const char *)bytes + offsets[i];
+        const uint32_t kl = (uint32_t)(offsets[i + 1] - offsets[i]);
+        const uint32_t *p = probe + 4 * i;
+        if ((p[2] & 0xffffu) && shf_get_uid_val_copy(shf, p[0]) == SHF_RET_KEY_FOUND) {
+            uint32_t stored_len;
+            memcpy(&stored_len, (const char *)shf_key_addr - sizeof(stored_len), sizeof(stored_len));
+            if (stored_len == kl && memcmp(shf_key_addr, k, kl) == 0) {
+                good += ref_val_is(i);
+                ++f;
+                continue;
+            }
+        }
+        shf_hash.u64[0] = hashes[2 * i];
+        shf_hash.u64[1] = hashes[2 * i + 1];
+        shf_hash_key = k;
+        shf_hash_key_len = kl;
+        good += shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND && ref_val_is(i);
+    }
+    if (seconds) *seconds = ref_now() - t0;
+    if (fast) *fast = f;
+    return good;
 }

@@ -3,19 +3,26 @@
 // Each kernel computes, for every key of a batch, exactly what the reference's
 // shf_make_hash() leaves in the thread-local SHF_HASH
 // (/root/reference/src/shf.c:450-462 -> murmurhash3.c:75-160), or the packed
-// UID parts that put/find derive from it (shf.c:800-803, :893-896).
+// UID parts that put/find derive from it (shf.c:800-803, :893-896), or that
+// hash's row pre-probe against a device copy of the store's rows (the row scan
+// of shf.c:886-922).
 //
 // Kernels (see DESIGN.md for the roofline of each):
 //   k_fixed16   key_len == 16: one lane per key, one 16-B coalesced load and one
 //               16-B coalesced store per lane. HBM-bound (32 B/key).
 //   k_tiled     key_len % 16 == 0, key_len >= 32 (the 256-B config): a wave owns
-//               64 keys; every round it stages 128 B of each key through LDS with
-//               fully-used 128-B segment loads, XOR-swizzled so the lane-per-key
-//               ds_read_b128 reads are bank-conflict free, and prefetches the next
-//               round into registers while hashing the current one.
+//               64 keys; every round it stages 8 or 16 pieces of 16 B of each key
+//               through LDS with fully-used segment loads, XOR-swizzled so the
+//               lane-per-key ds_read_b128 reads are bank-conflict free.
+//   k_span      variable-length keys and most other fixed lengths: a wave owns a
+//               tile of 64 consecutive keys = one contiguous span, fetched with
+//               1-KiB raw buffer loads, staged in LDS, hashed lane-per-key.
 //   k_generic   any length, fixed or variable (offset array): one lane per key,
 //               64-B per-lane bursts of dword-aligned loads, funnel-shifted with
 //               v_alignbyte_b32 for unaligned key starts.
+//   k_probe_hashes  row pre-probe of precomputed hashes.
+// Every hashing kernel takes its output as a Sink (kernels.h): 16-B hashes,
+// 8-B UID parts, or 16-B probe records (+ optional hashes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -103,6 +110,8 @@ __device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const
 }
 
 // Probe precomputed hashes: one lane per key.
+// (A wave-cooperative variant -- 8 lanes per row, matches gathered with
+// ballots and ds_bpermute -- measured 3.9x slower: profiles/r1/ab_probe_coop_vs_lane_*.txt.)
 __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ hashes, uint64_t n, Sink sink) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -114,38 +123,21 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 // ---------------------------------------------------------------------------
 // key_len == 16
 // ---------------------------------------------------------------------------
-#ifndef SHFHB_F16_UNROLL
-#define SHFHB_F16_UNROLL 1  // keys per lane per grid-stride step (2 and 4 measured no better)
-#endif
-#ifndef SHFHB_F16_GRID_CAP  // one key per lane up to 2^28 keys: 6.36 vs 5.16 TB/s at 100M keys
-#define SHFHB_F16_GRID_CAP (1u << 20)  // against a 8192-block grid-stride loop (profiles/r1/ab_fixed16.txt)
-#endif
+// One key per lane and as many workgroups as keys need: no grid-stride loop
+// (6.36 vs 5.16 TB/s at 100M keys against a 8192-block grid-stride loop,
+// profiles/r1/ab_fixed16.txt; a loop that runs once measured the same,
+// profiles/r1/ab_fixed16_noloop_*.txt). OUT = kOutProbe is the fused
+// hash + row pre-probe.
 template <int OUT>
 __global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
                                                  Sink sink) {
-  constexpr int U = SHFHB_F16_UNROLL;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // U keys per lane at a stride of the grid: U coalesced 16-B loads in flight
-  for (; i + (U - 1) * stride < n; i += U * stride) {
-    u32x4 k[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) k[u] = __builtin_nontemporal_load(&keys[i + u * stride]);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      State s{seed, seed};
-      body_block(s, pack64(k[u].x, k[u].y), pack64(k[u].z, k[u].w));
-      finish(s, 16);
-      store_result<OUT>(sink, i + u * stride, s);
-    }
-  }
-  for (; i < n; i += stride) {
-    const u32x4 k = __builtin_nontemporal_load(&keys[i]);
-    State s{seed, seed};
-    body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
-    finish(s, 16);
-    store_result<OUT>(sink, i, s);
-  }
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 k = __builtin_nontemporal_load(&keys[i]);
+  State s{seed, seed};
+  body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
+  finish(s, 16);
+  store_result<OUT>(sink, i, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -669,8 +661,8 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   }
   switch (kernel) {
     case kKernelFixed16:
-      if (key_len != 16 || !al16) return hipErrorInvalidValue;
-      hipLaunchKernelGGL(k_fixed16<OUT>, dim3(grid_for(n, 256, SHFHB_F16_GRID_CAP)), dim3(256), 0, st,
+      if (key_len != 16 || !al16 || (n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(k_fixed16<OUT>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                          reinterpret_cast<const u32x4*>(keys), n, seed, sink);
       break;
     case kKernelTiled: {

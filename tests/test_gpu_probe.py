@@ -172,3 +172,48 @@ def test_probe_full_size_config_b(torch, oracle):
     finally:
         idx.close()
 
+
+
+@pytest.mark.skipif(reference_lib() is None, reason="oracle/_ref not built")
+def test_probe_drives_reference_get(torch, tmp_path_factory):
+    """f3 end to end: the reference fills a store; its rows go to HBM; the GPU
+    hashes and probes a get batch; the reference's get then serves every stored
+    key through the probe's uid (shf_get_uid_val_copy + key compare) with the
+    right value, and falls back to its ordinary get for the rest."""
+    import ctypes
+    import tempfile
+    import time
+
+    lib = reference_lib()
+    n_put, n_abs = 200_000, 20_000
+    n = n_put + n_abs
+    lens = splitmix_lengths(n, 8, 200, 31)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]), 32), dtype=np.uint8)
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        shf = lib.ref_store_open(d.encode(), b"probe_get")
+        assert shf
+        try:
+            assert lib.ref_store_put(shf, data.ctypes.data, off.ctypes.data, n_put) == n_put
+            ts = np.empty(256 * 2048, dtype=np.uint32)
+            rows = np.zeros(4096 * 65536, dtype=np.uint8)
+            slots = lib.ref_export_rows(shf, ts.ctypes.data, rows.ctypes.data, 4096)
+            assert slots >= 256
+            idx = hb.RowIndex(slots, ts, rows[: slots * 65536])
+            t0 = time.perf_counter()
+            rec, h = hb.probe_var(idx, _dev(torch, data), _dev(torch, off.view(np.int64)), hashes=True)
+            torch.cuda.synchronize()
+            gpu_s = time.perf_counter() - t0
+            rec_np, h_np = _u32(rec), _u64(h)
+            fast, sec = ctypes.c_uint64(), ctypes.c_double()
+            good = lib.ref_store_get_probed(shf, data.ctypes.data, off.ctypes.data, n, rec_np.ctypes.data,
+                                            h_np.ctypes.data, ctypes.byref(fast), ctypes.byref(sec))
+            assert good == n_put and fast.value == n_put
+            sec_plain = ctypes.c_double()
+            assert lib.ref_store_get_plain(shf, data.ctypes.data, off.ctypes.data, n, ctypes.byref(sec_plain)) == n_put
+            print("get loop: reference %.1f ns/key, probe-driven %.1f ns/key (+ GPU %.1f ms incl. copies)" % (
+                1e9 * sec_plain.value / n, 1e9 * sec.value / n, 1e3 * gpu_s))
+            idx.close()
+        finally:
+            lib.ref_store_close(shf)

@@ -129,3 +129,42 @@ def test_synthetic_index_torch_equals_numpy(oracle):
     assert np.array_equal(a[0], b[0].numpy().view(np.uint32))
     assert np.array_equal(a[1], b[1].numpy())
     assert a[2:] == b[2:]
+
+
+@pytest.mark.skipif(reference_lib() is None, reason="oracle/_ref not built")
+def test_probe_records_drive_reference_get(oracle):
+    """The INTEGRATION.md §6 get loop on the reference's own store, fed with
+    oracle probe records (tests/test_gpu_probe.py feeds it the GPU's)."""
+    import ctypes
+    import tempfile
+
+    lib = reference_lib()
+    n_put, n_abs = 30_000, 5_000
+    n = n_put + n_abs
+    lens = splitmix_lengths(n, 8, 120, 41)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]), 42), dtype=np.uint8)
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        shf = lib.ref_store_open(d.encode(), b"probe_get_cpu")
+        assert shf
+        try:
+            assert lib.ref_store_put(shf, data.ctypes.data, off.ctypes.data, n_put) == n_put
+            ts = np.empty(256 * 2048, dtype=np.uint32)
+            rows = np.zeros(1024 * 65536, dtype=np.uint8)
+            slots = lib.ref_export_rows(shf, ts.ctypes.data, rows.ctypes.data, 1024)
+            assert slots >= 256
+            h = oracle.hash_var(data, off)
+            rec = oracle.probe(h, ts, rows[: slots * 65536])
+            fast, sec = ctypes.c_uint64(), ctypes.c_double()
+            good = lib.ref_store_get_probed(shf, data.ctypes.data, off.ctypes.data, n, rec.ctypes.data, h.ctypes.data,
+                                            ctypes.byref(fast), ctypes.byref(sec))
+            assert good == n_put and fast.value == n_put
+            # a stale probe (candidate uid pointing at another key) is caught by the key compare
+            bad = rec.copy()
+            bad[:n_put:2] = rec[1:n_put:2][: bad[:n_put:2].shape[0]]
+            good2 = lib.ref_store_get_probed(shf, data.ctypes.data, off.ctypes.data, n, bad.ctypes.data,
+                                             h.ctypes.data, ctypes.byref(fast), ctypes.byref(sec))
+            assert good2 == n_put and fast.value < n_put
+        finally:
+            lib.ref_store_close(shf)

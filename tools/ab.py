@@ -34,7 +34,7 @@ def build(name, flags, outdir):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--variant", action="append", required=True, help="name=-Dflags ...")
-    p.add_argument("--workload", default="fixed256", choices=["fixed16", "fixed256", "var", "fixedL"])
+    p.add_argument("--workload", default="fixed256", choices=["fixed16", "fixed256", "var", "fixedL", "probe16", "probeh"])
     p.add_argument("--key-len", type=int, default=37)
     p.add_argument("--n", type=int, default=20_000_000)
     p.add_argument("--rounds", type=int, default=6)
@@ -55,7 +55,25 @@ def main():
         libs[name] = hb.load(build(name, flags, outdir))
     dev = torch.device("cuda:0")
     n = a.n
-    if a.workload in ("fixed16", "fixed256", "fixedL"):
+    out_shape = (n, 2)
+    if a.workload in ("probe16", "probeh"):  # hash+probe / probe of hashes against an index of all keys
+        from sharedhashfile_amd.rowindex import synthetic_index
+
+        keys = device_random_bytes(n * 16, 1, dev)
+        h = hb.hash_fixed(keys, 16)
+        ts, rows, n_slots, _ = synthetic_index(h, tabs_per_win=16)
+        index = hb.RowIndex(n_slots, ts, rows)  # one handle; every variant reads the same device index
+        del ts, rows
+        out_shape = (n, 4)
+        if a.workload == "probe16":
+            per_key = 16 + 128 + 16
+            call = lambda lib, out: lib.shf_probe_batch_fixed_kernel_async(index.handle, keys.data_ptr(), 16, n, 12345,
+                                                                           None, out.data_ptr(), a.kernel, None)
+        else:
+            per_key = 16 + 128 + 16
+            call = lambda lib, out: lib.shf_probe_batch_hashes_async(index.handle, h.data_ptr(), n, out.data_ptr(),
+                                                                     None)
+    elif a.workload in ("fixed16", "fixed256", "fixedL"):
         L = {"fixed16": 16, "fixed256": 256, "fixedL": a.key_len}[a.workload]
         keys = device_random_bytes(n * L, 1, dev)
         per_key = L + 16
@@ -71,7 +89,8 @@ def main():
         per_key = float(off[-1].item()) / n + 24
         call = lambda lib, out: lib.shf_hash_batch_var_kernel_async(data.data_ptr(), off.data_ptr(), n, 12345,
                                                                      out.data_ptr(), a.kernel, None)
-    outs = {k: torch.empty((n, 2), dtype=torch.int64, device=dev) for k in libs}
+    outs = {k: torch.empty(out_shape, dtype=torch.int64 if out_shape[1] == 2 else torch.int32, device=dev)
+            for k in libs}
     for k, lib in libs.items():
         assert call(lib, outs[k]) == 0
     torch.cuda.synchronize()
