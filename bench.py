@@ -54,10 +54,11 @@ def parse():
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
     p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var,probe16 (default: all)")
     p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
-    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic"])
+    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-threads", type=int, default=16, help="threads for cpu_baseline.all_cores (0/1: skip)")
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
                    help="auto: at N=1 run two short rocprofv3 --pmc child passes for HBM bytes")
     p.add_argument("--host-inclusive", action="store_true",
@@ -128,9 +129,9 @@ def make_workloads(args, dev, rank):
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         del lens
         wl.append(Workload("var", n, total / n + 8 + 16,
-                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3}[args.var_kernel]:
+                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]:
                            hb.hash_var(d, o, out=out, kernel=vk),
-                           "k_span" if args.var_kernel != "generic" else "k_generic", "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
+                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding
         # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +
@@ -256,9 +257,24 @@ def cpu_baseline(args):
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
-    return {"value": n * passes / dt, "unit": "keys/s", "cores": 1, "kind": kind,
-            "sample": "%d passes x 1M 16-B keys (test.9 loop shape, hash only), %.1f s, %s; host %s (%d cpus visible)"
-                      % (passes, dt, what, model, os.cpu_count() or 0)}
+    out = {"value": n * passes / dt, "unit": "keys/s", "cores": 1, "kind": kind,
+           "sample": "%d passes x 1M 16-B keys (test.9 loop shape, hash only), %.1f s, %s; host %s (%d cpus visible)"
+                     % (passes, dt, what, model, os.cpu_count() or 0)}
+    # SURVEY.md s8(d) config A also asks for all cores: the box's CPU share for one GPU is 16 threads
+    threads = args.cpu_threads
+    if threads > 1:
+        mt_passes = max(1, int(passes * threads / 4))  # ~1/4 of the single-core time if it scales
+        if ref is not None:
+            dt_mt = ref.ref_bench_make_hash_loop(keys.ctypes.data, L, n, mt_passes, threads, ctypes.byref(fold))
+        else:
+            t0 = time.perf_counter()
+            for _ in range(mt_passes):
+                o.hash_fixed(keys, L, threads=threads)
+            dt_mt = time.perf_counter() - t0
+        out["all_cores"] = {"value": n * mt_passes / dt_mt, "unit": "keys/s", "cores": threads,
+                            "sample": "%d passes x 1M 16-B keys over %d threads (even key ranges), %.1f s"
+                                      % (mt_passes, threads, dt_mt)}
+    return out
 
 
 # ---------------------------------------------------------------------------

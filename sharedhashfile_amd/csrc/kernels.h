@@ -10,7 +10,14 @@ namespace shfhb {
 // kOutProbe: 16-B shf_probe records (row pre-probe), plus the
 // hashes when Sink::hash_out is set.
 enum OutMode { kOutHash = 0, kOutUid = 1, kOutProbe = 2 };
-enum KernelChoice { kKernelAuto = 0, kKernelFixed16 = 1, kKernelTiled = 2, kKernelGeneric = 3, kKernelSpan = 4 };
+enum KernelChoice {
+  kKernelAuto = 0,
+  kKernelFixed16 = 1,
+  kKernelTiled = 2,
+  kKernelGeneric = 3,
+  kKernelSpan = 4,
+  kKernelRound = 5
+};
 
 // Where a kernel's per-key result goes (passed by value as a kernel argument).
 struct Sink {

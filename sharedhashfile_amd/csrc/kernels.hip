@@ -546,6 +546,157 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
   return s;
 }
 
+// ---------------------------------------------------------------------------
+// Round kernel: variable-length keys, streamed 128 B per key per round.
+// One wave (= one workgroup) owns 64 consecutive keys. Round r stages, for
+// every key still running, the 9 aligned 16-B pieces that hold its bytes
+// [128r, 128r + 128) (counted from the key's first aligned piece) into a
+// 144-B LDS window per key, loaded cooperatively (lane l of load instruction q
+// fetches piece (64q + l) % 9 of key (64q + l) / 9: runs of 144 contiguous
+// bytes per key), and prefetches round r + 1 into registers while each lane
+// hashes its own key's 8 blocks of round r out of its window. LDS per wave is
+// ~10 KiB (k_span needs the whole 64-key span, 20 KiB), so twice as many
+// tiles are in flight per CU. A tile with a key longer than kVrMaxRounds
+// rounds is hashed straight from HBM (hash_bytes).
+// ---------------------------------------------------------------------------
+constexpr int kVrPieces = 9;                     // 16-B pieces per key per round
+constexpr uint32_t kVrWindow = kVrPieces * 16u;  // 144 B
+constexpr uint32_t kVrMaxRounds = 64;            // keys up to 8 KiB in the staged path
+#ifndef SHFHB_VR_NT
+#define SHFHB_VR_NT 0
+#endif
+
+// Hash the blocks of round r of a key from its LDS window: window bytes
+// [sh16, sh16 + 128) are key bytes [128r, 128r + 128). All 36 dwords the
+// round can touch are read at once (the k_tiled lesson: ILP over LDS latency),
+// the 8 blocks' k1/k2 mixes are computed unconditionally and the chain step is
+// kept only for real blocks (no divergent branches); the tail block, if it
+// falls in this round, is re-read from the window afterwards.
+__device__ __forceinline__ void vround_blocks(State& s, const uint32_t* win, uint32_t sh16, uint32_t first_block,
+                                              uint32_t nb, uint32_t rem) {
+  const uint32_t sh = sh16 & 3u;
+  const uint32_t* w = win + (sh16 >> 2);
+  uint32_t x[33];
+#pragma unroll
+  for (int d = 0; d < 33; ++d) x[d] = w[d];  // up to window byte 3*4 + 32*4 + 3 < 144 + slack
+#pragma unroll
+  for (uint32_t t = 0; t < 8; ++t) {
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(x[4 * t + 1], x[4 * t + 0], sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(x[4 * t + 2], x[4 * t + 1], sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(x[4 * t + 3], x[4 * t + 2], sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4 * t + 4], x[4 * t + 3], sh);
+    State n = s;
+    body_block(n, pack64(d0, d1), pack64(d2, d3));
+    const bool real = first_block + t < nb;
+    s.h1 = real ? n.h1 : s.h1;
+    s.h2 = real ? n.h2 : s.h2;
+  }
+  if (rem != 0u && nb >= first_block && nb < first_block + 8u) {
+    const uint32_t* v = w + 4u * (nb - first_block);
+    const uint32_t y0 = v[0], y1 = v[1], y2 = v[2], y3 = v[3], y4 = v[4];
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(y1, y0, sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(y2, y1, sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(y3, y2, sh);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(y4, y3, sh);
+    const uint64_t t1 = pack64(d0, d1) & low_bytes_mask(rem);
+    const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
+    tail_block(s, t1, t2, rem);
+  }
+}
+
+constexpr uint32_t kVrStageBytes = (64u * kVrPieces + 2u) * 16u;  // windows + read slack
+constexpr uint32_t kVrLdsBytes = kVrStageBytes + 2u * 64u * 4u;      // + per-key tables
+
+// Round-streamed hashing of one 64-key tile (this lane: key `key`, bytes
+// [start, start + len) of `bytes`). `lds`: kVrLdsBytes, 16-B aligned, private
+// to this wave. Wave-uniform control flow.
+template <int OUT>
+__device__ __forceinline__ void vround_tile(const uint8_t* bytes, uint64_t key, bool valid, uint64_t start,
+                                            uint32_t len, uint32_t seed, const Sink& sink, uint8_t* lds) {
+  u32x4* stage = reinterpret_cast<u32x4*>(lds);
+  uint32_t* s_rel = reinterpret_cast<uint32_t*>(lds + kVrStageBytes);  // key's first aligned piece - tile's
+  uint32_t* s_end = s_rel + 64;  // bytes from that piece to the key's end (0: nothing to load)
+  const uint32_t lane = __lane_id();
+  const uint64_t addr = reinterpret_cast<uintptr_t>(bytes) + start;
+  const uint32_t sh16 = (uint32_t)(addr & 15u);
+  const uint32_t nb = len >> 4, rem = len & 15u;
+  const uint32_t my_rounds = (nb + (rem ? 1u : 0u) + 7u) >> 3;
+  uint32_t R = my_rounds;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) R = max(R, (uint32_t)__shfl_xor((int)R, m));
+  R = __builtin_amdgcn_readfirstlane(R);
+  State s{seed, seed};
+  if (R > kVrMaxRounds) {  // wave-uniform: a key over 8 KiB in this tile
+    if (valid) store_result<OUT>(sink, key, hash_bytes(bytes + start, len, seed));
+    return;
+  }
+  // the tile's first aligned piece (lane 0 holds the lowest start; offsets are monotone)
+  const uint64_t a16 = addr & ~(uint64_t)15;
+  const uint64_t tile0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a16) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a16 >> 32)) << 32);
+  s_rel[lane] = (uint32_t)(a16 - tile0);  // < 64 x 8 KiB + 16
+  s_end[lane] = len ? sh16 + len : 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // static load mapping: instruction q, lane -> (key lk, piece lp)
+  uint32_t lrel[kVrPieces], lend[kVrPieces];
+#pragma unroll
+  for (int q = 0; q < kVrPieces; ++q) {
+    const uint32_t idx = 64u * q + lane;
+    const uint32_t lk = idx / kVrPieces, lp = idx % kVrPieces;
+    lrel[q] = s_rel[lk] + 16u * lp;
+    lend[q] = s_end[lk] > 16u * lp ? s_end[lk] - 16u * lp : 0u;  // bytes left from this piece to the key's end
+  }
+  // a global (not flat) view: flat loads also count against lgkmcnt, so every
+  // LDS wait would drain the prefetch as well
+  auto fetch = [&](uint32_t r, u32x4 (&reg)[kVrPieces]) {
+#pragma unroll
+    for (int q = 0; q < kVrPieces; ++q) {
+      reg[q] = u32x4{0u, 0u, 0u, 0u};
+      if (128u * r < lend[q])  // the piece starts inside the key: its aligned 16 B cannot leave the key's page
+#if SHFHB_VR_NT
+        reg[q] = __builtin_nontemporal_load(reinterpret_cast<g_u32x4*>(tile0 + lrel[q] + 128u * r));
+#else  // keep lines in L2: the window's last piece is the next round's first
+        reg[q] = *reinterpret_cast<g_u32x4*>(tile0 + lrel[q] + 128u * r);
+#endif
+    }
+  };
+  u32x4 nxt[kVrPieces];
+  fetch(0, nxt);
+  const uint32_t* win = reinterpret_cast<const uint32_t*>(stage) + lane * (kVrWindow / 4);
+  for (uint32_t r = 0; r < R; ++r) {
+#pragma unroll
+    for (int q = 0; q < kVrPieces; ++q) stage[64 * q + lane] = nxt[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (r + 1 < R) fetch(r + 1, nxt);
+    if (r < my_rounds) vround_blocks(s, win, sh16, 8u * r, nb, rem);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  finish(s, len);
+  if (valid) store_result<OUT>(sink, key, s);
+}
+
+template <int OUT>
+__global__ __launch_bounds__(64) void k_vround(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
+                                               uint64_t off_base, uint64_t n, uint32_t seed, Sink sink) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kVrLdsBytes];
+  const uint64_t key = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+  const bool valid = key < n;
+  uint64_t start = 0;
+  uint32_t len = 0;
+  if (valid) {
+    const uint64_t o0 = offsets[key], o1 = offsets[key + 1];
+    start = o0 - off_base;
+    len = (uint32_t)(o1 - o0);
+  }
+  vround_tile<OUT>(bytes, key, valid, start, len, seed, sink, lds);
+}
+
 template <int OUT, bool VAR, int PIECES>
 __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
@@ -563,6 +714,8 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
       const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
       store_result<OUT>(sink, ti.key, hash_lds(span_lds, p, ti.len, seed));
     }
+  } else if constexpr (VAR) {  // span over the window: stream it in rounds (vround_tile) instead
+    vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, reinterpret_cast<uint8_t*>(span_lds));
   } else if (ti.valid) {
     store_result<OUT>(sink, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
   }
@@ -698,6 +851,13 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
   if (kernel == kKernelGeneric) {
     hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, sink);
+    return hipGetLastError();
+  }
+  if (kernel == kKernelRound) {
+    const uint64_t tiles = (n + 63) / 64;
+    if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_vround<OUT>, dim3((unsigned)tiles), dim3(64), 0, st, reinterpret_cast<const uint8_t*>(bytes),
+                       offsets, off_base, n, seed, sink);
     return hipGetLastError();
   }
   return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st);

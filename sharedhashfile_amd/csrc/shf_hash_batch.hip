@@ -237,6 +237,22 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   return SHF_HB_OK;
 }
 
+// The host path knows each chunk's key bytes, so it picks the variable-length
+// kernel by mean key length (tools/sweep_var.sh, profiles/r1/sweep_var/, GB/s):
+//   mean  36 B (U[8,64]):   generic 4003, round 2804, span 2516
+//   mean  68 B (U[8,128]):  round 3769, generic 3501, span 3206
+//   mean 132 B (U[8,256]):  round 3807 = span 3805
+//   mean 260 B (U[8,512]):  span 4148, round 3776
+//   mean 1028 B (U[8,2048]): round 3797, span 3247 (64-key spans overflow its window)
+// Device-resident calls cannot see the lengths and use AUTO (span).
+int var_kernel_for(uint64_t bytes, uint64_t keys) {
+  const uint64_t mean = keys ? bytes / keys : 0;
+  if (mean < 48) return shfhb::kKernelGeneric;
+  if (mean < 128) return shfhb::kKernelRound;
+  if (mean <= 300) return shfhb::kKernelSpan;
+  return shfhb::kKernelRound;
+}
+
 // Host-memory variable-length pipeline: chunks of whole keys up to kStageBytes
 // of key bytes (a single larger key gets a chunk of its own).
 int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
@@ -281,7 +297,8 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], in_pinned ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
                                   c->st[s]));
     HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
-    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, out_sink(c->d_out[s]), shfhb::kOutHash, c->st[s]));
+    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, out_sink(c->d_out[s]), shfhb::kOutHash, c->st[s],
+                             var_kernel_for(nb, cnt)));
     HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
                           hipMemcpyDeviceToHost, c->st[s]));
     HB_TRY(hipEventRecord(c->done[s], c->st[s]));
@@ -484,7 +501,8 @@ int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offse
                                     shf_hash128* d_out, int kernel, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
-  if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC)
+  if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC &&
+      kernel != SHF_HB_KERNEL_ROUND)
     return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
 }

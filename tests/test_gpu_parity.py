@@ -46,7 +46,7 @@ def fixed_kernels(key_len, aligned=True):
     return ks
 
 
-VAR_KERNELS = [0, 3, 4]  # AUTO (= SPAN), GENERIC, SPAN
+VAR_KERNELS = [0, 3, 4, 5]  # AUTO, GENERIC, SPAN, ROUND
 
 
 # ---------------------------------------------------------------------------
@@ -236,6 +236,27 @@ def test_var_near_window_and_deferred_mixed(hb, dev, oracle):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("shift", [0, 5, 13])
+def test_var_round_edges(hb, dev, oracle, shift):
+    """k_vround: keys at the staged-path limit (8192 B = 64 rounds) and just past
+    it (HBM fallback), lengths 0..17 and 127..129 around round and piece
+    boundaries, empty keys at the very end of the buffer, unaligned starts."""
+    rng = np.random.default_rng(77 + shift)
+    pieces = []
+    for _ in range(3000):
+        pieces.append(rng.choice([0, 1, 15, 16, 17, 127, 128, 129, 143, 144, 145, 255, 256, 257]))
+    lens = np.array(pieces, dtype=np.uint64)
+    lens[640:704] = rng.choice([8175, 8176, 8177, 8191, 8192], size=64)  # one tile at the limit
+    lens[1280] = 8193  # this tile falls back
+    lens[-5:] = 0  # empty keys at the end
+    off = np.zeros(lens.size + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]) + shift, 5 + shift), dtype=np.uint8)
+    want = oracle.hash_var(data[shift:], off)
+    got = u64(hb.hash_var(d_u8(data, dev), d_off(off + np.uint64(shift), dev), kernel=5))
+    assert np.array_equal(got, want)
+
+
 def test_var_long_keys(hb, dev, oracle):
     lens = np.array([65537, 1 << 20, 3, (1 << 20) + 15, 0, 100000], dtype=np.uint64)
     off = np.zeros(lens.size + 1, dtype=np.uint64)
@@ -321,6 +342,18 @@ def test_host_var_multi_chunk(hb, dev, oracle):
     want = oracle.hash_var(data, off)
     assert np.array_equal(hb.hash_var_host(data, off), want)
     assert np.array_equal(hb.hash_var_host(data, off, n_devices=0), want)
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 40), (8, 128), (200, 400), (300, 3000)])
+def test_host_var_kernel_by_mean_length(hb, dev, oracle, lo, hi):
+    """The host path picks generic / round / span / round by mean key length."""
+    rng = np.random.default_rng(lo + hi)
+    n = 40_000
+    lens = rng.integers(lo, hi + 1, size=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]) + 3, lo + 1), dtype=np.uint8)[3:]
+    assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
 
 
 def test_host_pinned_buffers(hb, dev, oracle):

@@ -23,6 +23,9 @@ sys.path.insert(0, ROOT)
 def build(name, flags, outdir):
     from sharedhashfile_amd import build as b
 
+    if not flags.strip() and os.path.exists(os.path.join(ROOT, "sharedhashfile_amd", "libshf_hash_batch.so")):
+        return os.path.join(ROOT, "sharedhashfile_amd", "libshf_hash_batch.so")  # the in-tree build as is
+
     so = os.path.join(outdir, "lib_%s.so" % name)
     cmd = [b.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
            "-I" + os.path.join(ROOT, "include")] + flags.split() + [os.path.join(b.CSRC, s) for s in b.SOURCES] + [
@@ -40,6 +43,8 @@ def main():
     p.add_argument("--rounds", type=int, default=6)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--kernel", type=int, default=0)
+    p.add_argument("--var-lo", type=int, default=8, help="var workload: key lengths U[var-lo, var-hi]")
+    p.add_argument("--var-hi", type=int, default=512)
     p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
     a = p.parse_args()
 
@@ -82,7 +87,7 @@ def main():
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(3)
-        lens = torch.randint(8, 513, (n,), generator=g, device=dev, dtype=torch.int64)
+        lens = torch.randint(a.var_lo, a.var_hi + 1, (n,), generator=g, device=dev, dtype=torch.int64)
         off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         torch.cumsum(lens, 0, out=off[1:])
         data = device_random_bytes(int(off[-1].item()), 2, dev)
