@@ -195,6 +195,14 @@ SHF_HB_API int shf_probe_batch_fixed_async(const shf_row_index *index, const voi
 SHF_HB_API int shf_probe_batch_var_async(const shf_row_index *index, const void *d_bytes,
                                          const uint64_t *d_offsets, uint64_t n, uint32_t seed,
                                          shf_hash128 *d_hashes, shf_probe *d_probe, void *hip_stream);
+/* Synchronous, like shf_hash_batch_fixed / _var: mem = SHF_HASH_MEM_DEVICE
+ * (every buffer in HBM) or SHF_HASH_MEM_HOST (keys, offsets, hashes and probes
+ * in host memory, pipelined through pinned staging like the hashing calls).
+ * hashes may be NULL. The index lives on the calling thread's current device. */
+SHF_HB_API int shf_probe_batch_fixed(const shf_row_index *index, const void *keys, uint32_t key_len, uint64_t n,
+                                     uint32_t seed, shf_hash128 *hashes, shf_probe *probes, int mem);
+SHF_HB_API int shf_probe_batch_var(const shf_row_index *index, const void *bytes, const uint64_t *offsets,
+                                   uint64_t n, uint32_t seed, shf_hash128 *hashes, shf_probe *probes, int mem);
 /* Probe precomputed hashes (n records on the device). */
 SHF_HB_API int shf_probe_batch_hashes_async(const shf_row_index *index, const shf_hash128 *d_hashes, uint64_t n,
                                             shf_probe *d_probe, void *hip_stream);

@@ -84,6 +84,8 @@ _SIGS = {
     "shf_probe_batch_fixed_async": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _VP],
     "shf_probe_batch_var_async": [_VP, _VP, _VP, _U64, _U32, _VP, _VP, _VP],
     "shf_probe_batch_hashes_async": [_VP, _VP, _U64, _VP, _VP],
+    "shf_probe_batch_fixed": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _INT],
+    "shf_probe_batch_var": [_VP, _VP, _VP, _U64, _U32, _VP, _VP, _INT],
     "shf_probe_batch_fixed_kernel_async": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _INT, _VP],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
@@ -356,6 +358,33 @@ def probe_hashes(index, hashes, out=None, stream=None):
                                              ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_probe_batch_hashes_async")
     return out
+
+
+def probe_fixed_host(index, keys, key_len=None, seed=SEED, hashes=False):
+    """Host buffers in and out: (n, 4) uint32 probe records (+ (n, 2) uint64 hashes)."""
+    keys = _np_u8(keys)
+    if key_len is None:
+        n, key_len = keys.shape
+    else:
+        n = keys.size // key_len if key_len else 0
+    rec = np.empty((n, 4), dtype=np.uint32)
+    h = np.empty((n, 2), dtype=np.uint64) if hashes else None
+    rc = load().shf_probe_batch_fixed(index.handle, keys.ctypes.data, key_len, n, seed,
+                                      h.ctypes.data if h is not None else None, rec.ctypes.data, MEM_HOST)
+    _check(rc, "shf_probe_batch_fixed")
+    return (rec, h) if hashes else rec
+
+
+def probe_var_host(index, data, offsets, seed=SEED, hashes=False):
+    data = _np_u8(data)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = max(offsets.size - 1, 0)
+    rec = np.empty((n, 4), dtype=np.uint32)
+    h = np.empty((n, 2), dtype=np.uint64) if hashes else None
+    rc = load().shf_probe_batch_var(index.handle, data.ctypes.data, offsets.ctypes.data, n, seed,
+                                    h.ctypes.data if h is not None else None, rec.ctypes.data, MEM_HOST)
+    _check(rc, "shf_probe_batch_var")
+    return (rec, h) if hashes else rec
 
 
 # ---------------------------------------------------------------------------

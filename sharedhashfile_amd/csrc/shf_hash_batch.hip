@@ -18,6 +18,14 @@
 #include "../../include/shf_hash_batch.h"
 #include "kernels.h"
 
+// Row index: device copies of a store's tab map and rows (shf_hash_batch.h).
+struct shf_row_index {
+  int dev = -1;
+  uint32_t* d_tab_slot = nullptr;
+  uint8_t* d_rows = nullptr;
+  uint64_t n_slots = 0;
+};
+
 namespace {
 
 thread_local int tls_last_hip = 0;
@@ -69,6 +77,9 @@ struct DevCtx {
   uint64_t* h_off[kSlots] = {nullptr, nullptr};
   uint64_t* d_off[kSlots] = {nullptr, nullptr};
   size_t key_cap = 0;  // records in h_out/d_out and offsets (+1) per slot
+  shf_probe* h_probe[kSlots] = {nullptr, nullptr};  // row pre-probe records (allocated on first use)
+  shf_probe* d_probe[kSlots] = {nullptr, nullptr};
+  size_t probe_cap = 0;
 };
 
 thread_local std::map<int, DevCtx*> tls_ctx;
@@ -114,11 +125,14 @@ void free_staging(DevCtx* c) {
     if (c->d_out[s]) (void)hipFree(c->d_out[s]);
     if (c->h_off[s]) (void)hipHostFree(c->h_off[s]);
     if (c->d_off[s]) (void)hipFree(c->d_off[s]);
+    if (c->h_probe[s]) (void)hipHostFree(c->h_probe[s]);
+    if (c->d_probe[s]) (void)hipFree(c->d_probe[s]);
     c->h_in[s] = c->d_in[s] = nullptr;
     c->h_out[s] = c->d_out[s] = nullptr;
     c->h_off[s] = c->d_off[s] = nullptr;
+    c->h_probe[s] = c->d_probe[s] = nullptr;
   }
-  c->in_cap = c->key_cap = 0;
+  c->in_cap = c->key_cap = c->probe_cap = 0;
 }
 
 // Release every context of this thread (worker threads of the *_multi calls).
@@ -160,6 +174,24 @@ int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys) {
   return SHF_HB_OK;
 }
 
+// Probe-record staging, key_cap records per slot (after ensure_staging).
+int ensure_probe_staging(DevCtx* c) {
+  if (c->probe_cap >= c->key_cap) return SHF_HB_OK;
+  for (int s = 0; s < kSlots; ++s) {
+    HB_TRY(hipStreamSynchronize(c->st[s]));
+    if (c->h_probe[s]) (void)hipHostFree(c->h_probe[s]);
+    if (c->d_probe[s]) (void)hipFree(c->d_probe[s]);
+    c->h_probe[s] = c->d_probe[s] = nullptr;
+  }
+  c->probe_cap = 0;
+  for (int s = 0; s < kSlots; ++s) {
+    HB_TRY(hipHostMalloc((void**)&c->h_probe[s], c->key_cap * sizeof(shf_probe), hipHostMallocDefault));
+    HB_TRY(hipMalloc((void**)&c->d_probe[s], c->key_cap * sizeof(shf_probe)));
+  }
+  c->probe_cap = c->key_cap;
+  return SHF_HB_OK;
+}
+
 // Caller host memory that is already page-locked (hipHostMalloc /
 // hipHostRegister): DMA straight from / into it, no staging copy.
 bool is_host_pinned(const void* p) {
@@ -191,30 +223,76 @@ void par_memcpy(void* dst, const void* src, size_t n) {
   for (auto& x : th) x.join();
 }
 
+// What a host pipeline writes: hashes and/or row pre-probe records.
+struct HostJob {
+  shf_hash128* hash = nullptr;
+  shf_probe* probe = nullptr;
+  const shf_row_index* index = nullptr;  // with probe
+};
+
 // One chunk in flight per slot; `pending` remembers where its results go.
 struct Pending {
   bool busy = false;
-  shf_hash128* dst = nullptr;  // nullptr: results were DMA'd straight to the caller
+  shf_hash128* hash = nullptr;  // nullptr: not requested, or DMA'd straight to the caller
+  shf_probe* probe = nullptr;
   uint64_t count = 0;
 };
 
 int drain_slot(DevCtx* c, int s, Pending& p) {
   if (!p.busy) return SHF_HB_OK;
   HB_TRY(hipEventSynchronize(c->done[s]));
-  if (p.dst) par_memcpy(p.dst, c->h_out[s], p.count * sizeof(shf_hash128));
+  if (p.hash) par_memcpy(p.hash, c->h_out[s], p.count * sizeof(shf_hash128));
+  if (p.probe) par_memcpy(p.probe, c->h_probe[s], p.count * sizeof(shf_probe));
   p.busy = false;
   return SHF_HB_OK;
 }
 
+// Kernel output of slot s for `job`.
+void job_sink(DevCtx* c, int s, const HostJob& job, shfhb::Sink* k, int* mode) {
+  *k = shfhb::Sink();
+  if (job.probe) {
+    k->out = c->d_probe[s];
+    k->hash_out = job.hash ? c->d_out[s] : nullptr;
+    k->tab_slot = job.index->d_tab_slot;
+    k->rows = job.index->d_rows;
+    k->n_slots = job.index->n_slots;
+    *mode = shfhb::kOutProbe;
+  } else {
+    k->out = c->d_out[s];
+    *mode = shfhb::kOutHash;
+  }
+}
+
+// Results of chunk [i0, i0 + cnt) back to the caller (straight into page-locked
+// caller memory, else into the slot's staging for drain_slot to copy).
+int job_d2h(DevCtx* c, int s, const HostJob& job, uint64_t i0, uint64_t cnt, bool hash_pinned, bool probe_pinned,
+            Pending* p) {
+  *p = Pending{true, nullptr, nullptr, cnt};
+  if (job.hash) {
+    HB_TRY(hipMemcpyAsync(hash_pinned ? job.hash + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
+                          hipMemcpyDeviceToHost, c->st[s]));
+    if (!hash_pinned) p->hash = job.hash + i0;
+  }
+  if (job.probe) {
+    HB_TRY(hipMemcpyAsync(probe_pinned ? job.probe + i0 : c->h_probe[s], c->d_probe[s], cnt * sizeof(shf_probe),
+                          hipMemcpyDeviceToHost, c->st[s]));
+    if (!probe_pinned) p->probe = job.probe + i0;
+  }
+  HB_TRY(hipEventRecord(c->done[s], c->st[s]));
+  return SHF_HB_OK;
+}
+
 // Host-memory fixed-length pipeline on the current device.
-int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out) {
+int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
   const uint64_t per = key_len ? std::max<uint64_t>(1, kStageBytes / key_len) : (uint64_t)1 << 22;
   const uint64_t chunk = std::min<uint64_t>(per, n);
   if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk))) return rc;
-  const bool in_pinned = is_host_pinned(keys), out_pinned = is_host_pinned(out);
+  if (job.probe && (rc = ensure_probe_staging(c))) return rc;
+  const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
+             probe_pinned = is_host_pinned(job.probe);
   Pending pend[kSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += chunk, ++idx) {
@@ -225,12 +303,11 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     const uint8_t* src = in_pinned ? keys + i0 * key_len : c->h_in[s];
     if (nb && !in_pinned) par_memcpy(c->h_in[s], keys + i0 * key_len, nb);
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], src, nb, hipMemcpyHostToDevice, c->st[s]));
-    HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, out_sink(c->d_out[s]), shfhb::kOutHash, c->st[s],
-                               shfhb::kKernelAuto));
-    HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
-                          hipMemcpyDeviceToHost, c->st[s]));
-    HB_TRY(hipEventRecord(c->done[s], c->st[s]));
-    pend[s] = Pending{true, out_pinned ? nullptr : out + i0, cnt};
+    shfhb::Sink k;
+    int mode = 0;
+    job_sink(c, s, job, &k, &mode);
+    HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto));
+    if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
   }
   for (int s = 0; s < kSlots; ++s)
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
@@ -255,12 +332,13 @@ int var_kernel_for(uint64_t bytes, uint64_t keys) {
 
 // Host-memory variable-length pipeline: chunks of whole keys up to kStageBytes
 // of key bytes (a single larger key gets a chunk of its own).
-int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
+int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
   const uint64_t max_keys = std::min<uint64_t>(n, (uint64_t)1 << 22);
-  const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets), out_pinned = is_host_pinned(out);
+  const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
+             hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
   Pending pend[kSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
@@ -286,6 +364,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
         if ((rc = drain_slot(c, s, pend[s]))) return rc;
       if ((rc = ensure_staging(c, std::max(nb, (size_t)1), need_keys))) return rc;
     }
+    if (job.probe && (rc = ensure_probe_staging(c))) return rc;
     const int s = (int)(idx % kSlots);
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
     if (nb && !in_pinned) par_memcpy(c->h_in[s], bytes + base, nb);
@@ -297,12 +376,11 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], in_pinned ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
                                   c->st[s]));
     HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
-    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, out_sink(c->d_out[s]), shfhb::kOutHash, c->st[s],
-                             var_kernel_for(nb, cnt)));
-    HB_TRY(hipMemcpyAsync(out_pinned ? out + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
-                          hipMemcpyDeviceToHost, c->st[s]));
-    HB_TRY(hipEventRecord(c->done[s], c->st[s]));
-    pend[s] = Pending{true, out_pinned ? nullptr : out + i0, cnt};
+    shfhb::Sink k;
+    int mode = 0;
+    job_sink(c, s, job, &k, &mode);
+    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, k, mode, c->st[s], var_kernel_for(nb, cnt)));
+    if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
     i0 = i1;
   }
   for (int s = 0; s < kSlots; ++s)
@@ -324,12 +402,18 @@ int drain_on_error(int rc) {
   return rc;
 }
 
-int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out) {
-  return drain_on_error(host_fixed_run(keys, key_len, n, seed, out));
+int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
+  return drain_on_error(host_fixed_run(keys, key_len, n, seed, job));
 }
 
-int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out) {
-  return drain_on_error(host_var_run(bytes, offsets, n, seed, out));
+int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job) {
+  return drain_on_error(host_var_run(bytes, offsets, n, seed, job));
+}
+
+HostJob hash_job(shf_hash128* out) {
+  HostJob j;
+  j.hash = out;
+  return j;
 }
 
 int check_var_lengths_host(const uint64_t* offsets, uint64_t n) {
@@ -379,17 +463,6 @@ bool fixed_kernel_fits(const void* d_keys, uint32_t key_len, int kernel) {
   }
 }
 
-// Row index: device copies of a store's tab map and rows (shf_hash_batch.h).
-}  // namespace
-
-struct shf_row_index {
-  int dev = -1;
-  uint32_t* d_tab_slot = nullptr;
-  uint8_t* d_rows = nullptr;
-  uint64_t n_slots = 0;
-};
-
-namespace {
 
 // Probe sink for `index` on the calling thread's current device.
 int probe_sink(const shf_row_index* index, void* d_probe, void* d_hashes, shfhb::Sink* sink) {
@@ -457,7 +530,7 @@ int shf_hash_batch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_
   if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   if (mem == SHF_HASH_MEM_DEVICE)
     return device_fixed(keys, key_len, n, seed, out_sink(out), shfhb::kOutHash, nullptr, shfhb::kKernelAuto, true);
-  if (mem == SHF_HASH_MEM_HOST) return host_fixed((const uint8_t*)keys, key_len, n, seed, out);
+  if (mem == SHF_HASH_MEM_HOST) return host_fixed((const uint8_t*)keys, key_len, n, seed, hash_job(out));
   return SHF_HB_ERR_ARG;
 }
 
@@ -485,7 +558,7 @@ int shf_hash_batch_var(const void* bytes, const uint64_t* offsets, uint64_t n, u
   if (mem == SHF_HASH_MEM_HOST) {
     int rc = check_var_lengths_host(offsets, n);
     if (rc) return rc;
-    return host_var((const uint8_t*)bytes, offsets, n, seed, out);
+    return host_var((const uint8_t*)bytes, offsets, n, seed, hash_job(out));
   }
   return SHF_HB_ERR_ARG;
 }
@@ -528,7 +601,7 @@ int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, u
   if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   const uint8_t* k = (const uint8_t*)keys;
   return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
-    return host_fixed(k ? k + lo * key_len : nullptr, key_len, hi - lo, seed, out + lo);
+    return host_fixed(k ? k + lo * key_len : nullptr, key_len, hi - lo, seed, hash_job(out + lo));
   });
 }
 
@@ -540,7 +613,7 @@ int shf_hash_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_
   if (rc) return rc;
   const uint8_t* b = (const uint8_t*)bytes;
   return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
-    return host_var(b, offsets + lo, hi - lo, seed, out + lo);
+    return host_var(b, offsets + lo, hi - lo, seed, hash_job(out + lo));
   });
 }
 
@@ -627,6 +700,40 @@ int shf_probe_batch_var_async(const shf_row_index* index, const void* d_bytes, c
   int rc = probe_sink(index, d_probe, d_hashes, &sink);
   if (rc) return rc;
   return device_var(d_bytes, d_offsets, n, seed, sink, shfhb::kOutProbe, (hipStream_t)hip_stream, false);
+}
+
+int shf_probe_batch_fixed(const shf_row_index* index, const void* keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                          shf_hash128* hashes, shf_probe* probes, int mem) {
+  if (n == 0) return SHF_HB_OK;
+  if (!probes || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  shfhb::Sink sink;
+  int rc = probe_sink(index, probes, hashes, &sink);
+  if (rc) return rc;
+  if (mem == SHF_HASH_MEM_DEVICE)
+    return device_fixed(keys, key_len, n, seed, sink, shfhb::kOutProbe, nullptr, shfhb::kKernelAuto, true);
+  if (mem != SHF_HASH_MEM_HOST) return SHF_HB_ERR_ARG;
+  HostJob job;
+  job.hash = hashes;
+  job.probe = probes;
+  job.index = index;
+  return host_fixed((const uint8_t*)keys, key_len, n, seed, job);
+}
+
+int shf_probe_batch_var(const shf_row_index* index, const void* bytes, const uint64_t* offsets, uint64_t n,
+                        uint32_t seed, shf_hash128* hashes, shf_probe* probes, int mem) {
+  if (n == 0) return SHF_HB_OK;
+  if (!probes || !offsets || !bytes) return SHF_HB_ERR_ARG;
+  shfhb::Sink sink;
+  int rc = probe_sink(index, probes, hashes, &sink);
+  if (rc) return rc;
+  if (mem == SHF_HASH_MEM_DEVICE) return device_var(bytes, offsets, n, seed, sink, shfhb::kOutProbe, nullptr, true);
+  if (mem != SHF_HASH_MEM_HOST) return SHF_HB_ERR_ARG;
+  if ((rc = check_var_lengths_host(offsets, n))) return rc;
+  HostJob job;
+  job.hash = hashes;
+  job.probe = probes;
+  job.index = index;
+  return host_var((const uint8_t*)bytes, offsets, n, seed, job);
 }
 
 int shf_probe_batch_hashes_async(const shf_row_index* index, const shf_hash128* d_hashes, uint64_t n,

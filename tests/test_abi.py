@@ -47,7 +47,12 @@ def test_record_layout_matches_shf_hash():
     # SHF_HASH: 16-byte packed union, u64[0]=h1, u64[1]=h2 (shf.private.h:180-185).
     src = ('#include <stddef.h>\n#include "shf_hash_batch.h"\n'
            '_Static_assert(sizeof(shf_hash128) == 16, "size");\n'
-           '_Static_assert(offsetof(shf_hash128, h2) == 8, "h2");\nint main(void){return 0;}\n')
+           '_Static_assert(offsetof(shf_hash128, h2) == 8, "h2");\n'
+           # shf_probe: {uid, pos, mask, tab, slot} = 4 u32 words as the kernels write them
+           '_Static_assert(sizeof(shf_probe) == 16, "probe");\n'
+           '_Static_assert(offsetof(shf_probe, pos) == 4 && offsetof(shf_probe, mask) == 8, "p1");\n'
+           '_Static_assert(offsetof(shf_probe, tab) == 10 && offsetof(shf_probe, slot) == 12, "p2");\n'
+           'int main(void){return 0;}\n')
     p = subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-x", "c", "-", "-o", "/dev/null"],
                        input=src.encode(), capture_output=True)
     assert p.returncode == 0, p.stderr.decode()
@@ -97,6 +102,10 @@ def test_argument_validation_needs_no_device(hb):
                                          out.ctypes.data, None) == hbmod.ERR_ARG
     assert lib.shf_probe_batch_hashes_async(None, out.ctypes.data, 4, out.ctypes.data, None) == hbmod.ERR_ARG
     assert lib.shf_probe_batch_hashes_async(None, None, 0, None, None) == hbmod.OK
+    assert lib.shf_probe_batch_fixed(None, keys.ctypes.data, 16, 4, 12345, None, out.ctypes.data,
+                                     hbmod.MEM_HOST) == hbmod.ERR_ARG
+    assert lib.shf_probe_batch_var(None, keys.ctypes.data, keys.ctypes.data, 2, 12345, None, None,
+                                   hbmod.MEM_HOST) == hbmod.ERR_ARG
     assert lib.shf_row_index_create(0, None) == hbmod.ERR_ARG
     assert lib.shf_row_index_create(1 << 22, ctypes.byref(ctypes.c_void_p())) == hbmod.ERR_ARG
     assert lib.shf_row_index_destroy(None) == hbmod.OK

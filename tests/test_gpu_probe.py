@@ -217,3 +217,46 @@ def test_probe_drives_reference_get(torch, tmp_path_factory):
             idx.close()
         finally:
             lib.ref_store_close(shf)
+
+
+def test_probe_host_memory_paths(torch, oracle, golden, golden_index):
+    """shf_probe_batch_fixed / _var with host buffers (pipelined through pinned
+    staging) and with device buffers (synchronous)."""
+    want = oracle.probe(golden["ref_hash"], golden["tab_slot"], golden["rows"])
+    rec, h = hb.probe_fixed_host(golden_index, golden["keys"], hashes=True)
+    assert np.array_equal(rec, want) and np.array_equal(h, golden["ref_hash"])
+    n = golden["keys"].shape[0]
+    off = np.arange(n + 1, dtype=np.uint64) * 16
+    assert np.array_equal(hb.probe_var_host(golden_index, golden["keys"].reshape(-1), off), want)
+    lib = hb.load()
+    d_keys = _dev(torch, golden["keys"])
+    d_rec = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+    assert lib.shf_probe_batch_fixed(golden_index.handle, d_keys.data_ptr(), 16, n, hb.SEED, None,
+                                     d_rec.data_ptr(), hb.MEM_DEVICE) == hb.OK
+    assert np.array_equal(_u32(d_rec), want)
+
+
+def test_probe_host_multi_chunk_var(torch, oracle):
+    """More key bytes than one 64 MiB staging chunk, variable lengths, pinned
+    output buffers (DMA'd straight into) and pageable ones."""
+    n = 400_000
+    lens = splitmix_lengths(n, 100, 400, 61)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)  # ~100 MB
+    data = np.frombuffer(splitmix_bytes(int(off[-1]), 62), dtype=np.uint8)
+    h = oracle.hash_var(data, off)
+    tab_slot, rows, n_slots, _ = synthetic_index(h, tabs_per_win=2, limit=n - 1000)
+    idx = hb.RowIndex(n_slots, tab_slot, rows)
+    try:
+        want = oracle.probe(h, tab_slot, rows)
+        rec, hh = hb.probe_var_host(idx, data, off, hashes=True)
+        assert np.array_equal(rec, want) and np.array_equal(hh, h)
+        lib = hb.load()
+        p_rec = torch.zeros((n, 4), dtype=torch.int32).pin_memory()
+        p_h = torch.zeros((n, 2), dtype=torch.int64).pin_memory()
+        assert lib.shf_probe_batch_var(idx.handle, data.ctypes.data, off.ctypes.data, n, hb.SEED, p_h.data_ptr(),
+                                       p_rec.data_ptr(), hb.MEM_HOST) == hb.OK
+        assert np.array_equal(p_rec.numpy().view(np.uint32), want)
+        assert np.array_equal(p_h.numpy().view(np.uint64), h)
+    finally:
+        idx.close()
