@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
     p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var,probe16 (default: all)")
     p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
-    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round"])
+    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round", "stream"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -92,6 +92,26 @@ class Workload:
         self.launch, self.kernel, self.desc = launch, kernel, desc
 
 
+def fast_launch(hb, keys, key_len, n, out, kernel, dev):
+    """The C-ABI launch with its ctypes arguments built once: a 50-us kernel must
+    not wait on per-call Python argument checks (hb.hash_fixed does the same call)."""
+    import ctypes
+
+    import torch
+
+    fn = hb.load().shf_hash_batch_fixed_kernel_async
+    argv = (ctypes.c_void_p(keys.data_ptr()), ctypes.c_uint32(key_len), ctypes.c_uint64(n),
+            ctypes.c_uint32(SEED), ctypes.c_void_p(out.data_ptr()), ctypes.c_int(kernel),
+            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+
+    def launch():
+        rc = fn(*argv)
+        if rc:
+            raise hb.ShfHashBatchError(rc, "shf_hash_batch_fixed_kernel_async")
+
+    return launch
+
+
 def make_workloads(args, dev, rank):
     import torch
 
@@ -106,8 +126,7 @@ def make_workloads(args, dev, rank):
         keys = device_random_bytes(n * 16, seed_base + 1, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         fk = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
-        wl.append(Workload("fixed16", n, 16 + 16,
-                           lambda k=keys, o=out, fk=fk: hb.hash_fixed(k, 16, out=o, kernel=fk),
+        wl.append(Workload("fixed16", n, 16 + 16, fast_launch(hb, keys, 16, n, out, fk, dev),
                            "k_fixed16", "%d fixed 16-B keys" % n))
     if "fixed256" in only:
         n = args.keys256
@@ -129,9 +148,9 @@ def make_workloads(args, dev, rank):
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         del lens
         wl.append(Workload("var", n, total / n + 8 + 16,
-                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]:
+                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5, "stream": 6}[args.var_kernel]:
                            hb.hash_var(d, o, out=out, kernel=vk),
-                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
+                           {"generic": "k_generic", "round": "k_vround", "span": "k_span", "stream": "k_vstream"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding
         # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +

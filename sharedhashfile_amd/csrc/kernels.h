@@ -16,7 +16,8 @@ enum KernelChoice {
   kKernelTiled = 2,
   kKernelGeneric = 3,
   kKernelSpan = 4,
-  kKernelRound = 5
+  kKernelRound = 5,
+  kKernelStream = 6
 };
 
 // Where a kernel's per-key result goes (passed by value as a kernel argument).

@@ -128,16 +128,42 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 // profiles/r1/ab_fixed16.txt; a loop that runs once measured the same,
 // profiles/r1/ab_fixed16_noloop_*.txt). OUT = kOutProbe is the fused
 // hash + row pre-probe.
+#ifndef SHFHB_F16_BLOCK
+#define SHFHB_F16_BLOCK 256
+#endif
+#ifndef SHFHB_F16_KPL
+#define SHFHB_F16_KPL 1  // keys per lane (strided by the block size)
+#endif
+#ifndef SHFHB_F16_NTSTORE
+#define SHFHB_F16_NTSTORE 0
+#endif
+constexpr uint32_t kF16Block = SHFHB_F16_BLOCK;
+constexpr uint32_t kF16Kpl = SHFHB_F16_KPL;
+
 template <int OUT>
-__global__ __launch_bounds__(256) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
-                                                 Sink sink) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const u32x4 k = __builtin_nontemporal_load(&keys[i]);
-  State s{seed, seed};
-  body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
-  finish(s, 16);
-  store_result<OUT>(sink, i, s);
+__global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
+                                                       Sink sink) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * (kF16Block * kF16Kpl) + threadIdx.x;
+  u32x4 k[kF16Kpl];
+#pragma unroll
+  for (uint32_t j = 0; j < kF16Kpl; ++j) {
+    const uint64_t i = i0 + j * kF16Block;
+    if (i < n) k[j] = __builtin_nontemporal_load(&keys[i]);
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kF16Kpl; ++j) {
+    const uint64_t i = i0 + j * kF16Block;
+    if (i >= n) return;
+    State s{seed, seed};
+    body_block(s, pack64(k[j].x, k[j].y), pack64(k[j].z, k[j].w));
+    finish(s, 16);
+    if constexpr (OUT == kOutHash && SHFHB_F16_NTSTORE) {
+      const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + i);
+    } else {
+      store_result<OUT>(sink, i, s);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -697,6 +723,145 @@ __global__ __launch_bounds__(64) void k_vround(const uint8_t* __restrict__ bytes
   vround_tile<OUT>(bytes, key, valid, start, len, seed, sink, lds);
 }
 
+// ---------------------------------------------------------------------------
+// Stream kernel: variable-length keys streamed 128 B per key per round through
+// the same 144-B LDS windows as k_vround, but a lane whose key ends claims the
+// next unclaimed key of its chunk instead of idling until the tile's longest
+// key is done. One wave (= one workgroup) owns a chunk of `chunk` consecutive
+// keys. The claim counter is wave-uniform (ballot + mbcnt, claims in key
+// order), and every lane holds the offsets of its next key one claim ahead, so
+// the round after a key ends is fetched without waiting on the offset array.
+// Rounds per 64 keys follow the mean key length, not the tile's longest key:
+// U[8,512] needs ~2.5 rounds per key against k_vround's 4 per 64-key tile.
+// Loads: as k_vround (lane l of instruction q fetches piece (64q+l) % 9 of the
+// key lane (64q+l) / 9 is working on), from a per-lane {piece, bytes left}
+// table rewritten every round. Addresses are 32-bit relative to the chunk's
+// first aligned piece; a chunk spanning 4 GiB or more is hashed per lane.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kVsLdsBytes = kVrStageBytes + 64u * 8u;  // windows + per-lane {piece, left}
+constexpr uint32_t kVsNone = 0xffffffffu;
+#ifndef SHFHB_VS_CHUNK
+#define SHFHB_VS_CHUNK 1024  // keys per wave
+#endif
+#ifndef SHFHB_VS_WAVES
+#define SHFHB_VS_WAVES 1  // launch-bounds waves per SIMD (4 would spill under hipcc 7.2)
+#endif
+
+struct VsKey {
+  uint32_t idx;  // key index within the chunk (kVsNone: no key)
+  uint32_t rel;  // its first byte, relative to the chunk's first aligned piece
+  uint32_t len;
+};
+
+// 128-B rounds a key occupies: its blocks plus the tail block, at least one
+// (an empty key still needs a round slot to be finished and stored).
+__device__ __forceinline__ uint32_t vs_rounds(uint32_t len) {
+  const uint32_t r = ((len >> 4) + ((len & 15u) ? 1u : 0u) + 7u) >> 3;
+  return r ? r : 1u;
+}
+
+template <int OUT>
+__global__ __launch_bounds__(64, SHFHB_VS_WAVES) void k_vstream(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
+                                                uint64_t off_base, uint64_t n, uint32_t chunk, uint32_t seed,
+                                                Sink sink) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kVsLdsBytes];
+  u32x4* stage = reinterpret_cast<u32x4*>(lds);
+  u32x2* table = reinterpret_cast<u32x2*>(lds + kVrStageBytes);
+  const uint32_t lane = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+  const uint32_t kn = (uint32_t)min<uint64_t>((uint64_t)chunk, n - c0);
+  const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
+  const uint64_t base = (b + (offsets[c0] - off_base)) & ~(uint64_t)15;
+  const uint64_t span = b + (offsets[c0 + kn] - off_base) - base;
+  if (span >= 0xfffff000ull) {  // wave-uniform: a chunk of 4 GiB or more, per-lane loads
+    for (uint32_t k = lane; k < kn; k += 64u) {
+      const uint64_t o0 = offsets[c0 + k], o1 = offsets[c0 + k + 1];
+      store_result<OUT>(sink, c0 + k, hash_bytes(bytes + (o0 - off_base), (uint32_t)(o1 - o0), seed));
+    }
+    return;
+  }
+  const uint32_t span32 = (uint32_t)span;
+  auto load_key = [&](uint32_t idx) {
+    VsKey k{kVsNone, 0u, 0u};
+    if (idx < kn) {
+      const uint64_t o0 = offsets[c0 + idx], o1 = offsets[c0 + idx + 1];
+      k.idx = idx;
+      k.rel = (uint32_t)(b + (o0 - off_base) - base);
+      k.len = (uint32_t)(o1 - o0);
+    }
+    return k;
+  };
+  // Publish this lane's next round (key k, round r) and fetch every lane's
+  // round into registers. Loads are clamped to the chunk's span, so even
+  // non-monotone offsets cannot send a load outside it.
+  u32x4 reg[kVrPieces];
+  auto fetch = [&](const VsKey& k, uint32_t r) {
+    uint32_t a = 0u, left = 0u;
+    if (k.idx != kVsNone) {
+      a = (k.rel & ~15u) + 128u * r;
+      left = (k.rel & 15u) + k.len - 128u * r;  // bytes from piece a to the key's end
+      left = a < span32 ? min(left, span32 - a) : 0u;
+    }
+    table[lane] = u32x2{a, left};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < kVrPieces; ++q) {
+      const uint32_t idx = 64u * q + lane;
+      const uint32_t lk = idx / kVrPieces, lp = idx - kVrPieces * lk;
+      const u32x2 t = table[lk];
+      reg[q] = u32x4{0u, 0u, 0u, 0u};
+      if (16u * lp < t.y) reg[q] = *reinterpret_cast<g_u32x4*>(base + t.x + 16u * lp);
+    }
+  };
+
+  VsKey cur = load_key(lane), nxt = load_key(64u + lane);
+  uint32_t cur_r = 0;
+  uint32_t next_free = min(kn, 128u);  // wave-uniform claim counter
+  const uint32_t* win = reinterpret_cast<const uint32_t*>(stage) + lane * (kVrWindow / 4);
+  fetch(cur, 0);
+  State s{seed, seed};
+  while (true) {
+#pragma unroll
+    for (int q = 0; q < kVrPieces; ++q) stage[64 * q + lane] = reg[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    const bool has = cur.idx != kVsNone;
+    const bool last = has && cur_r + 1u == vs_rounds(cur.len);
+    // The next round: this key's next 128 B, or (when it ends now) the next
+    // key, whose replacement is claimed here and loaded a round ahead.
+    const bool take = !has || last;
+    VsKey up = take ? nxt : cur;
+    const uint32_t up_r = take ? 0u : cur_r + 1u;
+    const bool claim = take && nxt.idx != kVsNone;
+    const uint64_t m = __ballot(claim);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (claim) nxt = load_key(next_free + rank);
+    next_free = min(kn, next_free + (uint32_t)__popcll(m));
+    const bool more = __ballot(up.idx != kVsNone) != 0ull;  // wave-uniform
+    if (more) fetch(up, up_r);
+
+    if (has) {
+      vround_blocks(s, win, cur.rel & 15u, 8u * cur_r, cur.len >> 4, cur.len & 15u);
+      if (last) {
+        finish(s, cur.len);
+        store_result<OUT>(sink, c0 + cur.idx, s);
+        s = State{seed, seed};
+      }
+    }
+    // every lane's window reads precede the next round's staging writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!more) break;
+    cur = up;
+    cur_r = up_r;
+  }
+}
+
 template <int OUT, bool VAR, int PIECES>
 __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
@@ -814,9 +979,12 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   }
   switch (kernel) {
     case kKernelFixed16:
-      if (key_len != 16 || !al16 || (n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
-      hipLaunchKernelGGL(k_fixed16<OUT>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+    {
+      constexpr uint64_t per_block = (uint64_t)kF16Block * kF16Kpl;
+      if (key_len != 16 || !al16 || (n + per_block - 1) / per_block > 0x7fffffffull) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(k_fixed16<OUT>, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(kF16Block), 0, st,
                          reinterpret_cast<const u32x4*>(keys), n, seed, sink);
+    }
       break;
     case kKernelTiled: {
       if (key_len < 32 || (key_len & 15u) || !al16) return hipErrorInvalidValue;
@@ -851,6 +1019,18 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
   if (kernel == kKernelGeneric) {
     hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, sink);
+    return hipGetLastError();
+  }
+  if (kernel == kKernelStream) {
+    static const uint32_t chunk = [] {
+      const char* e = getenv("SHF_HB_STREAM_CHUNK");  // a tuning knob, read once
+      const long v = e ? atol(e) : 0;
+      return (v >= 64 && v <= (1 << 20)) ? (uint32_t)v : (uint32_t)SHFHB_VS_CHUNK;
+    }();
+    const uint64_t waves = (n + chunk - 1) / chunk;
+    if (waves > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_vstream<OUT>, dim3((unsigned)waves), dim3(64), 0, st,
+                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, chunk, seed, sink);
     return hipGetLastError();
   }
   if (kernel == kKernelRound) {

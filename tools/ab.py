@@ -23,6 +23,9 @@ sys.path.insert(0, ROOT)
 def build(name, flags, outdir):
     from sharedhashfile_amd import build as b
 
+    if flags.startswith("@"):  # prebuilt variant (tools/ab.py --prebuild on the CPU host)
+        return os.path.join(ROOT, flags[1:])
+
     if not flags.strip() and os.path.exists(os.path.join(ROOT, "sharedhashfile_amd", "libshf_hash_batch.so")):
         return os.path.join(ROOT, "sharedhashfile_amd", "libshf_hash_batch.so")  # the in-tree build as is
 
@@ -46,12 +49,23 @@ def main():
     p.add_argument("--var-lo", type=int, default=8, help="var workload: key lengths U[var-lo, var-hi]")
     p.add_argument("--var-hi", type=int, default=512)
     p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
+    p.add_argument("--graph", action="store_true", help="time `reps` launches captured in one HIP graph")
+    p.add_argument("--prebuild", default="", help="build every name=-Dflags variant into this dir and exit")
     a = p.parse_args()
+    if a.prebuild:
+        os.makedirs(a.prebuild, exist_ok=True)
+        for v in a.variant:
+            name, _, flags = v.partition("=")
+            print(build(name, flags, a.prebuild))
+        return
 
     import torch
 
     import sharedhashfile_amd as hb
     from sharedhashfile_amd.keygen import device_random_bytes
+
+    def cs():  # the current stream's handle (a capture stream inside torch.cuda.graph)
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     outdir = tempfile.mkdtemp(prefix="shfhb_ab_")
     libs = {}
@@ -73,7 +87,7 @@ def main():
         if a.workload == "probe16":
             per_key = 16 + 128 + 16
             call = lambda lib, out: lib.shf_probe_batch_fixed_kernel_async(index.handle, keys.data_ptr(), 16, n, 12345,
-                                                                           None, out.data_ptr(), a.kernel, None)
+                                                                           None, out.data_ptr(), a.kernel, cs())
         else:
             per_key = 16 + 128 + 16
             call = lambda lib, out: lib.shf_probe_batch_hashes_async(index.handle, h.data_ptr(), n, out.data_ptr(),
@@ -83,7 +97,7 @@ def main():
         keys = device_random_bytes(n * L, 1, dev)
         per_key = L + 16
         call = lambda lib, out: lib.shf_hash_batch_fixed_kernel_async(keys.data_ptr(), L, n, 12345, out.data_ptr(),
-                                                                       a.kernel, None)
+                                                                       a.kernel, cs())
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(3)
@@ -93,7 +107,7 @@ def main():
         data = device_random_bytes(int(off[-1].item()), 2, dev)
         per_key = float(off[-1].item()) / n + 24
         call = lambda lib, out: lib.shf_hash_batch_var_kernel_async(data.data_ptr(), off.data_ptr(), n, 12345,
-                                                                     out.data_ptr(), a.kernel, None)
+                                                                     out.data_ptr(), a.kernel, cs())
     outs = {k: torch.empty(out_shape, dtype=torch.int64 if out_shape[1] == 2 else torch.int32, device=dev)
             for k in libs}
     for k, lib in libs.items():
@@ -110,14 +124,26 @@ def main():
         outs["copy_ref"] = None
         call_orig = call
         call = lambda lib, out: (dst_c.copy_(src_c), 0)[1] if lib is None else call_orig(lib, out)
+    graphs = {}
+    if a.graph:
+        for k, lib in libs.items():
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(a.reps):
+                    call(lib, outs[k])
+            graphs[k] = g
+        torch.cuda.synchronize()
     times = {k: [] for k in libs}
     for r in range(a.rounds):
         for k, lib in libs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record()
-            for _ in range(a.reps):
-                call(lib, outs[k])
+            if k in graphs:
+                graphs[k].replay()
+            else:
+                for _ in range(a.reps):
+                    call(lib, outs[k])
             e1.record()
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.reps)
