@@ -17,7 +17,8 @@ enum KernelChoice {
   kKernelGeneric = 3,
   kKernelSpan = 4,
   kKernelRound = 5,
-  kKernelStream = 6
+  kKernelStream = 6,
+  kKernelSpan2 = 7
 };
 
 // Where a kernel's per-key result goes (passed by value as a kernel argument).
