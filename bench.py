@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
     p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var,probe16 (default: all)")
     p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
-    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round", "stream", "span2"])
+    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -148,9 +148,9 @@ def make_workloads(args, dev, rank):
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         del lens
         wl.append(Workload("var", n, total / n + 8 + 16,
-                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5, "stream": 6, "span2": 7}[args.var_kernel]:
+                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]:
                            hb.hash_var(d, o, out=out, kernel=vk),
-                           {"generic": "k_generic", "round": "k_vround", "span": "k_span", "stream": "k_vstream", "span2": "k_span2"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
+                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding
         # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +

@@ -127,13 +127,10 @@ SHF_HB_API int shf_hash_batch_var_multi(const void *bytes, const uint64_t *offse
 #define SHF_HB_KERNEL_GENERIC 3 /* any key_len, any alignment, per-lane loads straight from HBM */
 #define SHF_HB_KERNEL_SPAN 4    /* key_len <= 318 (fixed) / any keys (var): LDS-staged spans */
 #define SHF_HB_KERNEL_ROUND 5   /* var only: keys streamed 128 B per round through LDS */
-#define SHF_HB_KERNEL_STREAM 6  /* var only: as ROUND, lanes claim the next key as theirs end */
-#define SHF_HB_KERNEL_SPAN2 7   /* var only: as SPAN, block mixes spread evenly over the lanes, then per-key chains */
 
 SHF_HB_API int shf_hash_batch_fixed_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                       shf_hash128 *d_out, int kernel, void *hip_stream);
-/* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_SPAN2, SHF_HB_KERNEL_ROUND,
- * SHF_HB_KERNEL_STREAM or SHF_HB_KERNEL_GENERIC */
+/* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_ROUND or SHF_HB_KERNEL_GENERIC */
 SHF_HB_API int shf_hash_batch_var_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                     uint32_t seed, shf_hash128 *d_out, int kernel, void *hip_stream);
 

@@ -35,8 +35,6 @@ KERNEL_TILED = 2
 KERNEL_GENERIC = 3
 KERNEL_SPAN = 4
 KERNEL_ROUND = 5
-KERNEL_STREAM = 6
-KERNEL_SPAN2 = 7
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libshf_hash_batch.so")

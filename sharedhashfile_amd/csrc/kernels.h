@@ -16,9 +16,7 @@ enum KernelChoice {
   kKernelTiled = 2,
   kKernelGeneric = 3,
   kKernelSpan = 4,
-  kKernelRound = 5,
-  kKernelStream = 6,
-  kKernelSpan2 = 7
+  kKernelRound = 5
 };
 
 // Where a kernel's per-key result goes (passed by value as a kernel argument).

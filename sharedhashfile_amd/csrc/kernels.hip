@@ -723,145 +723,6 @@ __global__ __launch_bounds__(64) void k_vround(const uint8_t* __restrict__ bytes
   vround_tile<OUT>(bytes, key, valid, start, len, seed, sink, lds);
 }
 
-// ---------------------------------------------------------------------------
-// Stream kernel: variable-length keys streamed 128 B per key per round through
-// the same 144-B LDS windows as k_vround, but a lane whose key ends claims the
-// next unclaimed key of its chunk instead of idling until the tile's longest
-// key is done. One wave (= one workgroup) owns a chunk of `chunk` consecutive
-// keys. The claim counter is wave-uniform (ballot + mbcnt, claims in key
-// order), and every lane holds the offsets of its next key one claim ahead, so
-// the round after a key ends is fetched without waiting on the offset array.
-// Rounds per 64 keys follow the mean key length, not the tile's longest key:
-// U[8,512] needs ~2.5 rounds per key against k_vround's 4 per 64-key tile.
-// Loads: as k_vround (lane l of instruction q fetches piece (64q+l) % 9 of the
-// key lane (64q+l) / 9 is working on), from a per-lane {piece, bytes left}
-// table rewritten every round. Addresses are 32-bit relative to the chunk's
-// first aligned piece; a chunk spanning 4 GiB or more is hashed per lane.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kVsLdsBytes = kVrStageBytes + 64u * 8u;  // windows + per-lane {piece, left}
-constexpr uint32_t kVsNone = 0xffffffffu;
-#ifndef SHFHB_VS_CHUNK
-#define SHFHB_VS_CHUNK 1024  // keys per wave
-#endif
-#ifndef SHFHB_VS_WAVES
-#define SHFHB_VS_WAVES 1  // launch-bounds waves per SIMD (4 would spill under hipcc 7.2)
-#endif
-
-struct VsKey {
-  uint32_t idx;  // key index within the chunk (kVsNone: no key)
-  uint32_t rel;  // its first byte, relative to the chunk's first aligned piece
-  uint32_t len;
-};
-
-// 128-B rounds a key occupies: its blocks plus the tail block, at least one
-// (an empty key still needs a round slot to be finished and stored).
-__device__ __forceinline__ uint32_t vs_rounds(uint32_t len) {
-  const uint32_t r = ((len >> 4) + ((len & 15u) ? 1u : 0u) + 7u) >> 3;
-  return r ? r : 1u;
-}
-
-template <int OUT>
-__global__ __launch_bounds__(64, SHFHB_VS_WAVES) void k_vstream(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
-                                                uint64_t off_base, uint64_t n, uint32_t chunk, uint32_t seed,
-                                                Sink sink) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kVsLdsBytes];
-  u32x4* stage = reinterpret_cast<u32x4*>(lds);
-  u32x2* table = reinterpret_cast<u32x2*>(lds + kVrStageBytes);
-  const uint32_t lane = threadIdx.x;
-  const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
-  const uint32_t kn = (uint32_t)min<uint64_t>((uint64_t)chunk, n - c0);
-  const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
-  const uint64_t base = (b + (offsets[c0] - off_base)) & ~(uint64_t)15;
-  const uint64_t span = b + (offsets[c0 + kn] - off_base) - base;
-  if (span >= 0xfffff000ull) {  // wave-uniform: a chunk of 4 GiB or more, per-lane loads
-    for (uint32_t k = lane; k < kn; k += 64u) {
-      const uint64_t o0 = offsets[c0 + k], o1 = offsets[c0 + k + 1];
-      store_result<OUT>(sink, c0 + k, hash_bytes(bytes + (o0 - off_base), (uint32_t)(o1 - o0), seed));
-    }
-    return;
-  }
-  const uint32_t span32 = (uint32_t)span;
-  auto load_key = [&](uint32_t idx) {
-    VsKey k{kVsNone, 0u, 0u};
-    if (idx < kn) {
-      const uint64_t o0 = offsets[c0 + idx], o1 = offsets[c0 + idx + 1];
-      k.idx = idx;
-      k.rel = (uint32_t)(b + (o0 - off_base) - base);
-      k.len = (uint32_t)(o1 - o0);
-    }
-    return k;
-  };
-  // Publish this lane's next round (key k, round r) and fetch every lane's
-  // round into registers. Loads are clamped to the chunk's span, so even
-  // non-monotone offsets cannot send a load outside it.
-  u32x4 reg[kVrPieces];
-  auto fetch = [&](const VsKey& k, uint32_t r) {
-    uint32_t a = 0u, left = 0u;
-    if (k.idx != kVsNone) {
-      a = (k.rel & ~15u) + 128u * r;
-      left = (k.rel & 15u) + k.len - 128u * r;  // bytes from piece a to the key's end
-      left = a < span32 ? min(left, span32 - a) : 0u;
-    }
-    table[lane] = u32x2{a, left};
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int q = 0; q < kVrPieces; ++q) {
-      const uint32_t idx = 64u * q + lane;
-      const uint32_t lk = idx / kVrPieces, lp = idx - kVrPieces * lk;
-      const u32x2 t = table[lk];
-      reg[q] = u32x4{0u, 0u, 0u, 0u};
-      if (16u * lp < t.y) reg[q] = *reinterpret_cast<g_u32x4*>(base + t.x + 16u * lp);
-    }
-  };
-
-  VsKey cur = load_key(lane), nxt = load_key(64u + lane);
-  uint32_t cur_r = 0;
-  uint32_t next_free = min(kn, 128u);  // wave-uniform claim counter
-  const uint32_t* win = reinterpret_cast<const uint32_t*>(stage) + lane * (kVrWindow / 4);
-  fetch(cur, 0);
-  State s{seed, seed};
-  while (true) {
-#pragma unroll
-    for (int q = 0; q < kVrPieces; ++q) stage[64 * q + lane] = reg[q];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    const bool has = cur.idx != kVsNone;
-    const bool last = has && cur_r + 1u == vs_rounds(cur.len);
-    // The next round: this key's next 128 B, or (when it ends now) the next
-    // key, whose replacement is claimed here and loaded a round ahead.
-    const bool take = !has || last;
-    VsKey up = take ? nxt : cur;
-    const uint32_t up_r = take ? 0u : cur_r + 1u;
-    const bool claim = take && nxt.idx != kVsNone;
-    const uint64_t m = __ballot(claim);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (claim) nxt = load_key(next_free + rank);
-    next_free = min(kn, next_free + (uint32_t)__popcll(m));
-    const bool more = __ballot(up.idx != kVsNone) != 0ull;  // wave-uniform
-    if (more) fetch(up, up_r);
-
-    if (has) {
-      vround_blocks(s, win, cur.rel & 15u, 8u * cur_r, cur.len >> 4, cur.len & 15u);
-      if (last) {
-        finish(s, cur.len);
-        store_result<OUT>(sink, c0 + cur.idx, s);
-        s = State{seed, seed};
-      }
-    }
-    // every lane's window reads precede the next round's staging writes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!more) break;
-    cur = up;
-    cur_r = up_r;
-  }
-}
-
 template <int OUT, bool VAR, int PIECES>
 __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
@@ -883,133 +744,6 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
     vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, reinterpret_cast<uint8_t*>(span_lds));
   } else if (ti.valid) {
     store_result<OUT>(sink, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Two-phase span kernel (variable lengths): the tile's span is staged exactly
-// as in k_span, then
-//   phase 1  the k1/k2 mixes (murmurhash3.c:97, :101; 4 of the block's 4 + 4
-//            multiplies) of EVERY body block of the tile, split evenly over the
-//            64 lanes: lane l mixes the contiguous run of flat blocks
-//            [l*B/64, (l+1)*B/64) of the tile's B blocks, walking from key to
-//            key, and writes each (m1, m2) back into the span in place, into
-//            the aligned 16-B slot its block starts in (blocks are disjoint
-//            16-B ranges, so no two share a slot);
-//   phase 2  each lane runs only the serial h1/h2 chain of its own key over
-//            those slots (slot floor(p/16) + j holds block j of the key at p),
-//            then the tail and fmix.
-// Only the cheap chain (~1/3 of a block's VALU cost) still runs for the tile's
-// longest key; k_span runs the whole block for it.
-// In-place safety: writing block X's slot overwrites only bytes of the flat
-// block before it (the slot's bytes below X's start) or of a key tail. Tails
-// are read into registers first; the previous block is either this lane's
-// (read earlier, LDS ops of a wave retire in order) or, for the first block of
-// a run, the previous lane's last one -- so each run's first slot is written
-// only after a barrier that ends phase 1.
-// LDS: the span window, then per-key tables {start, blocks, blocks end}.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kSpan2Tables = 3u * 64u * 4u;
-constexpr uint32_t kSpan2Cap = kSpanAlloc - kSpanPad - kSpan2Tables;  // 19648 B
-
-template <int OUT>
-__global__ __launch_bounds__(64, 4) void k_span2(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
-                                                 uint64_t off_base, uint64_t n, uint32_t seed, Sink sink) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  const uint32_t lane = threadIdx.x;
-  const SpanTile<true> ti =
-      span_finish<true>(bytes, off_base, 0, n, span_load<true>(offsets, n, blockIdx.x, lane), lane);
-  if (ti.span16 > kSpan2Cap) {  // wave-uniform: stream the tile in rounds instead
-    vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, reinterpret_cast<uint8_t*>(span_lds));
-    return;
-  }
-  {
-    u32x4 reg[kSpanPiecesMax];
-    span_fetch<kSpanPiecesMax>(reg, ti.base, ti.span16, lane);
-    span_stage<kSpanPiecesMax>(span_lds, reg, ti.span16, lane);
-  }
-  uint32_t* t_p = span_lds + (kSpanAlloc - kSpan2Tables) / 4;  // key start in the span
-  uint32_t* t_nb = t_p + 64;                                     // body blocks
-  uint32_t* t_e = t_nb + 64;                                     // inclusive prefix sum of blocks
-  const uint32_t p = ti.valid ? (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base) : 0u;
-  const uint32_t len = ti.valid ? ti.len : 0u;
-  const uint32_t nb = len >> 4, rem = len & 15u;
-  uint32_t e = nb;  // inclusive scan of nb over the wave
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)e, d);
-    if (lane >= (uint32_t)d) e += t;
-  }
-  const uint32_t B = (uint32_t)__builtin_amdgcn_readlane((int)e, 63);
-  t_p[lane] = p;
-  t_nb[lane] = nb;
-  t_e[lane] = e;
-  __syncthreads();  // the staged span and the tables
-
-  // the tail bytes (murmurhash3.c:109-138), before phase 1 may overwrite them
-  uint64_t t1 = 0, t2 = 0;
-  if (rem) {
-    const uint32_t q = p + 16u * nb, sh = q & 3u;
-    const uint32_t* w = span_lds + (q >> 2);
-    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-    t1 = pack64(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh)) &
-         low_bytes_mask(rem);
-    t2 = rem > 8 ? (pack64(__builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)) &
-                    low_bytes_mask(rem - 8))
-                 : 0ull;
-  }
-  __syncthreads();
-
-  // phase 1: this lane's run of flat blocks [r0, r1)
-  const uint32_t r0 = (lane * B) >> 6, r1 = ((lane + 1u) * B) >> 6;
-  u32x4 first = {0u, 0u, 0u, 0u};
-  uint32_t first_slot = 0xffffffffu;
-  if (r1 > r0) {
-    // owner of r0: the first key whose blocks end past it (t_e is non-decreasing)
-    uint32_t lo = 0;
-#pragma unroll
-    for (uint32_t step = 32; step >= 1; step >>= 1)
-      if (t_e[lo + step - 1] <= r0) lo += step;
-    uint32_t k = lo;
-    uint32_t kp = t_p[k], knb = t_nb[k];
-    uint32_t j = r0 - (t_e[k] - knb);
-    for (uint32_t b = r0; b < r1; ++b) {
-      const uint32_t addr = kp + 16u * j, sh = addr & 3u;
-      const uint32_t* w = span_lds + (addr >> 2);
-      uint64_t m1, m2;
-      mix_dwords(w[0], w[1], w[2], w[3], w[4], sh, m1, m2);
-      const u32x4 v = {(uint32_t)m1, (uint32_t)(m1 >> 32), (uint32_t)m2, (uint32_t)(m2 >> 32)};
-      if (b == r0) {
-        first = v;
-        first_slot = addr >> 4;
-      } else {
-        reinterpret_cast<u32x4*>(span_lds)[addr >> 4] = v;
-      }
-      if (++j == knb && b + 1 < r1) {  // next key with blocks
-        do {
-          ++k;
-          knb = t_nb[k];
-        } while (knb == 0u && k < 63u);
-        kp = t_p[k];
-        j = 0;
-      }
-    }
-  }
-  __syncthreads();
-  if (first_slot != 0xffffffffu) reinterpret_cast<u32x4*>(span_lds)[first_slot] = first;
-  __syncthreads();
-
-  // phase 2: the chain of this lane's key over its mixed slots
-  if (ti.valid) {
-    State s{seed, seed};
-    const u32x4* slot = reinterpret_cast<const u32x4*>(span_lds) + (p >> 4);
-    for (uint32_t j = 0; j < nb; ++j) {
-      const u32x4 v = slot[j];
-      chain_block(s, pack64(v.x, v.y), pack64(v.z, v.w));
-    }
-    if (rem) tail_block(s, t1, t2, rem);
-    finish(s, len);
-    store_result<OUT>(sink, ti.key, s);
   }
 }
 
@@ -1146,25 +880,6 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
   if (kernel == kKernelGeneric) {
     hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, sink);
-    return hipGetLastError();
-  }
-  if (kernel == kKernelSpan2) {
-    const uint64_t tiles = (n + 63) / 64;
-    if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_span2<OUT>, dim3((unsigned)tiles), dim3(64), kSpanAlloc, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, sink);
-    return hipGetLastError();
-  }
-  if (kernel == kKernelStream) {
-    static const uint32_t chunk = [] {
-      const char* e = getenv("SHF_HB_STREAM_CHUNK");  // a tuning knob, read once
-      const long v = e ? atol(e) : 0;
-      return (v >= 64 && v <= (1 << 20)) ? (uint32_t)v : (uint32_t)SHFHB_VS_CHUNK;
-    }();
-    const uint64_t waves = (n + chunk - 1) / chunk;
-    if (waves > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_vstream<OUT>, dim3((unsigned)waves), dim3(64), 0, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, chunk, seed, sink);
     return hipGetLastError();
   }
   if (kernel == kKernelRound) {

@@ -575,8 +575,7 @@ int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offse
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC &&
-      kernel != SHF_HB_KERNEL_ROUND && kernel != SHF_HB_KERNEL_STREAM &&
-      kernel != SHF_HB_KERNEL_SPAN2)
+      kernel != SHF_HB_KERNEL_ROUND)
     return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
 }

@@ -46,7 +46,7 @@ def fixed_kernels(key_len, aligned=True):
     return ks
 
 
-VAR_KERNELS = [0, 3, 4, 5, 6, 7]  # AUTO, GENERIC, SPAN, ROUND, STREAM, SPAN2
+VAR_KERNELS = [0, 3, 4, 5]  # AUTO, GENERIC, SPAN, ROUND
 
 
 # ---------------------------------------------------------------------------
