@@ -103,6 +103,10 @@ def load(path=None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError("libshf_hash_batch.so not built (%s); run python -m sharedhashfile_amd.build" % p)
+    try:  # torch first: its bundled libamdhip64 (SONAME libamdhip64.so.7) then serves this library too,
+        import torch  # noqa: F401  so one HIP runtime owns every stream, event and buffer of the process
+    except ImportError:
+        pass
     lib = ctypes.CDLL(p)
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
