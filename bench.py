@@ -38,6 +38,7 @@ sys.path.insert(0, ROOT)
 METRIC = "keys hashed/s device-resident (16 B & 256 B keys) + GiB/s vs HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E peak (spec)
 SEED = 12345
+WARMUP_MIN_S = 0.25  # untimed warmup floor per workload (seconds of GPU work)
 
 # algorithmic bytes per key = key bytes read + 16-byte SHF_HASH
 # written (+ 8-byte offset read for variable-length keys).
@@ -50,6 +51,8 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--keys16", type=int, default=10_000_000, help="configs[1]: 16-B keys per GPU")
+    p.add_argument("--keys1b", type=int, default=1_000_000_000,
+                   help="configs[4]: 16-B keys for the whole job, split over the GPUs (strong scaling)")
     p.add_argument("--keys256", type=int, default=100_000_000, help="configs[2]: 256-B keys per GPU")
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
     p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var,probe16 (default: all)")
@@ -65,6 +68,8 @@ def parse():
                    help="also time the pinned host->device->host path (reported, never `value`)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="backend for the barrier/max-reduce only (gloo: multi-rank rehearsal on one GPU)")
+    p.add_argument("--warmup-min-s", type=float, default=WARMUP_MIN_S,
+                   help="keep warming up (untimed) until this many seconds of the workload have run")
     p.add_argument("--quiet", action="store_true")
     return p.parse_args()
 
@@ -112,13 +117,13 @@ def fast_launch(hb, keys, key_len, n, out, kernel, dev):
     return launch
 
 
-def make_workloads(args, dev, rank):
+def make_workloads(args, dev, rank, world=1):
     import torch
 
     import sharedhashfile_amd as hb
     from sharedhashfile_amd.keygen import device_random_bytes
 
-    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed256", "var", "probe16"}
+    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed256", "var", "probe16", "shard1b"}
     wl = []
     seed_base = 0x5348460000000001 + 1000 * rank
     if "fixed16" in only:
@@ -128,6 +133,18 @@ def make_workloads(args, dev, rank):
         fk = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
         wl.append(Workload("fixed16", n, 16 + 16, fast_launch(hb, keys, 16, n, out, fk, dev),
                            "k_fixed16", "%d fixed 16-B keys" % n))
+    if "shard1b" in only:
+        # configs[4]: 1B 16-B keys split evenly over the job's GPUs (strong scaling:
+        # 1B / world keys on this rank, contiguous index range, no collective).
+        total = args.keys1b
+        lo, hi = total * rank // world, total * (rank + 1) // world
+        n = hi - lo
+        keys = device_random_bytes(n * 16, seed_base + 6, dev)
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        w = Workload("shard1b", n, 16 + 16, fast_launch(hb, keys, 16, n, out, 0, dev),
+                     "k_fixed16", "%d 16-B keys split over %d GPU(s): keys [%d, %d) on rank %d" % (total, world, lo, hi, rank))
+        w.job_keys = total
+        wl.append(w)
     if "fixed256" in only:
         n = args.keys256
         keys = device_random_bytes(n * 256, seed_base + 2, dev)
@@ -173,14 +190,22 @@ def make_workloads(args, dev, rank):
     return wl
 
 
-def time_workload(w, steps, warmup, dist):
+def time_workload(w, steps, warmup, dist, warmup_min_s=WARMUP_MIN_S):
     """Returns (wall seconds for `steps` steps, max over ranks; mean per-launch
     kernel seconds from HIP events on the launch stream)."""
     import torch
 
     stream = torch.cuda.current_stream()  # the stream every launch goes to (hb passes it to the library)
-    for _ in range(warmup):
+    # W warmup steps, continued (untimed) until the GPU has run this workload
+    # for WARMUP_MIN_S: after seconds of host-side setup the clocks start low,
+    # and 10 steps of a 50-us kernel are not enough to bring them up.
+    t_w = time.perf_counter()
+    done = 0
+    while done < warmup or time.perf_counter() - t_w < warmup_min_s:
         w.launch()
+        done += 1
+        if done >= warmup and done % 16 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
@@ -191,8 +216,10 @@ def time_workload(w, steps, warmup, dist):
     for _ in range(steps):
         w.launch()
     ev1.record(stream)
+    t_enq = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    w.enqueue_s = t_enq - t0  # host time to enqueue the steps (diagnostic)
     if dist:
         dist.barrier()
     elapsed = t1 - t0
@@ -311,7 +338,7 @@ def collect_traffic(args, kernel_sym):
         outdir = tempfile.mkdtemp(prefix="shfhb_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
                sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--only", "fixed16",
-               "--no-cpu", "--traffic", "off", "--quiet", "--keys16", str(args.keys16)]
+               "--no-cpu", "--traffic", "off", "--quiet", "--keys16", str(args.keys16), "--warmup-min-s", "0"]
         try:
             subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            cwd=os.environ.get("TMPDIR", "/tmp"))
@@ -356,11 +383,11 @@ def main():
         dist = tdist
     hb.check_device()
 
-    wl = make_workloads(args, dev, rank)
+    wl = make_workloads(args, dev, rank, world)
     results = {}
     for w in wl:
-        elapsed, per_launch = time_workload(w, args.steps, args.warmup, dist)
-        keys_total = w.n * world * args.steps
+        elapsed, per_launch = time_workload(w, args.steps, args.warmup, dist, args.warmup_min_s)
+        keys_total = getattr(w, "job_keys", w.n * world) * args.steps
         results[w.name] = {
             "value": keys_total / elapsed,
             "ms_per_step": 1e3 * elapsed / args.steps,
@@ -369,9 +396,11 @@ def main():
             "bytes_per_key": w.bytes_per_key,
             "kernel": w.kernel,
             "desc": w.desc,
+            "enqueue_us_per_step": 1e6 * w.enqueue_s / args.steps,
         }
-        log(args, "[bench] %s: %.3f Gkeys/s, %.1f us/launch, %.0f GB/s" % (
-            w.name, results[w.name]["value"] / 1e9, per_launch * 1e6, results[w.name]["achieved_gbs"]))
+        log(args, "[bench] %s: %.3f Gkeys/s, %.1f us/launch, %.0f GB/s, host enqueue %.1f us/step" % (
+            w.name, results[w.name]["value"] / 1e9, per_launch * 1e6, results[w.name]["achieved_gbs"],
+            1e6 * w.enqueue_s / args.steps))
 
     if rank == 0:
         head = results.get("fixed16") or next(iter(results.values()))
@@ -397,6 +426,8 @@ def main():
                                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                             "frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4),
                                             "bytes_per_key": round(r["bytes_per_key"], 2)}}
+            if name == "shard1b":
+                secondary[name]["scaling"] = "strong"
         line = {
             "metric": METRIC,
             "value": head["value"],
