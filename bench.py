@@ -136,8 +136,10 @@ def make_workloads(args, dev, rank, world=1):
     if "shard1b" in only:
         # configs[4]: 1B 16-B keys split evenly over the job's GPUs (strong scaling:
         # 1B / world keys on this rank, contiguous index range, no collective).
+        from sharedhashfile_amd.shard import shard_range
+
         total = args.keys1b
-        lo, hi = total * rank // world, total * (rank + 1) // world
+        lo, hi = shard_range(total, rank, world)
         n = hi - lo
         keys = device_random_bytes(n * 16, seed_base + 6, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
@@ -236,8 +238,9 @@ def time_workload(w, steps, warmup, dist, warmup_min_s=WARMUP_MIN_S):
 
 def time_host_inclusive(args, n=10_000_000):
     """Host buffers in and out (SHF_HASH_MEM_HOST): H2D keys + kernel + D2H
-    hashes, pipelined in 64 MiB chunks on two streams. Pageable buffers are
-    staged through pinned memory; page-locked ones are DMA'd directly."""
+    hashes, pipelined in SHF_HB_STAGE_MB chunks, SHF_HB_SLOTS in flight on their
+    own streams. Pageable buffers are staged through pinned memory; page-locked
+    ones are DMA'd directly."""
     import torch
 
     import sharedhashfile_amd as hb

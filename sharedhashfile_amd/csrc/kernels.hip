@@ -17,6 +17,10 @@
 //   k_span      variable-length keys and most other fixed lengths: a wave owns a
 //               tile of 64 consecutive keys = one contiguous span, fetched with
 //               1-KiB raw buffer loads, staged in LDS, hashed lane-per-key.
+//   k_span_sorted  (SHFHB_SPAN_SORT_W > 1) the variable-length span path with W
+//               waves per workgroup hashing its 64 W keys in block-count order.
+//   k_vround    variable-length keys streamed 128 B per key per round through
+//               144-B LDS windows (short / very long keys, k_span's overflow).
 //   k_generic   any length, fixed or variable (offset array): one lane per key,
 //               64-B per-lane bursts of dword-aligned loads, funnel-shifted with
 //               v_alignbyte_b32 for unaligned key starts.
@@ -55,42 +59,68 @@ typedef __attribute__((address_space(1))) const uint32_t g_u32;
 constexpr uint32_t kProbeNone = 0xffffffffu;  // SHF_UID_NONE (shf.h:354) / no slot
 constexpr uint32_t kRowsPerTabShift = 16;     // 512 rows x 128 B = 64 KiB per slot
 
-__device__ __forceinline__ u32x4 probe_row(const Sink& k, const State& s) {
+// Two steps, so that the row loads of several keys can be in flight together:
+// probe_locate (the 4-B tab_slot lookup) and probe_scan (the row's 8 x 16-B
+// loads and 16 compares). The row loads are unconditional: a key whose tab is
+// not indexed scans a stand-in (the first 128 B of the tab map, always mapped)
+// and its result is discarded.
+struct ProbeLoc {
+  uint32_t win, tab2, row, want, e;
+};
+
+__device__ __forceinline__ ProbeLoc probe_locate(const Sink& k, const State& s) {
+  ProbeLoc p;
   const uint32_t lo = (uint32_t)s.h1;
-  const uint32_t win = lo & 0xffu;
-  const uint32_t tab2 = (lo >> 16) & 0x7ffu;
-  const uint32_t row = (uint32_t)(s.h1 >> 32) & 0x1ffu;
-  const uint32_t rnd = (uint32_t)s.h2 & 0x1fffffu;
-  const uint32_t e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.tab_slot))[(win << 11) | tab2];
-  u32x4 rec = {kProbeNone, 0u, 0xffffu << 16, kProbeNone};
-  if (e != kProbeNone && (uint64_t)(e >> 11) < k.n_slots) {
-    const uint32_t slot = e >> 11;
-    const g_u32x4* r = reinterpret_cast<const g_u32x4*>(reinterpret_cast<uintptr_t>(k.rows) +
-                                                       ((uint64_t)slot << kRowsPerTabShift) + (row << 7));
-    u32x4 v[8];
+  p.win = lo & 0xffu;
+  p.tab2 = (lo >> 16) & 0x7ffu;
+  p.row = (uint32_t)(s.h1 >> 32) & 0x1ffu;
+  p.want = p.tab2 | (((uint32_t)s.h2 & 0x1fffffu) << 11);
+  p.e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.tab_slot))[(p.win << 11) | p.tab2];
+  return p;
+}
+
+__device__ __forceinline__ u32x4 probe_scan(const Sink& k, const ProbeLoc& p) {
+  const uint32_t slot = p.e >> 11;
+  const bool indexed = p.e != kProbeNone && (uint64_t)slot < k.n_slots;
+  const uintptr_t at = indexed ? reinterpret_cast<uintptr_t>(k.rows) + ((uint64_t)slot << kRowsPerTabShift) +
+                                     (p.row << 7)
+                               : reinterpret_cast<uintptr_t>(k.tab_slot);
+  const g_u32x4* r = reinterpret_cast<const g_u32x4*>(at);
+  u32x4 v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = r[q];
-    const uint32_t want = tab2 | (rnd << 11);
-    uint32_t mask = 0, pos = 0, first = 0;
+  for (int q = 0; q < 8; ++q) v[q] = r[q];
+  uint32_t mask = 0, pos = 0, first = 0;
 #pragma unroll
-    for (int q = 7; q >= 0; --q) {  // descending: the lowest matching ref is written last
-      if (v[q].w != 0u && v[q].z == want) {
-        mask |= 2u << (2 * q);
-        pos = v[q].w;
-        first = 2 * q + 1;
-      }
-      if (v[q].y != 0u && v[q].x == want) {
-        mask |= 1u << (2 * q);
-        pos = v[q].y;
-        first = 2 * q;
-      }
+  for (int q = 7; q >= 0; --q) {  // descending: the lowest matching ref is written last
+    if (v[q].w != 0u && v[q].z == p.want) {
+      mask |= 2u << (2 * q);
+      pos = v[q].w;
+      first = 2 * q + 1;
     }
-    rec.x = mask ? (win | (tab2 << 8) | (row << 19) | (first << 28)) : kProbeNone;
+    if (v[q].y != 0u && v[q].x == p.want) {
+      mask |= 1u << (2 * q);
+      pos = v[q].y;
+      first = 2 * q;
+    }
+  }
+  u32x4 rec = {kProbeNone, 0u, 0xffffu << 16, kProbeNone};
+  if (indexed) {
+    rec.x = mask ? (p.win | (p.tab2 << 8) | (p.row << 19) | (first << 28)) : kProbeNone;
     rec.y = pos;
-    rec.z = mask | ((e & 0x7ffu) << 16);
+    rec.z = mask | ((p.e & 0x7ffu) << 16);
     rec.w = slot;
   }
   return rec;
+}
+
+__device__ __forceinline__ u32x4 probe_row(const Sink& k, const State& s) { return probe_scan(k, probe_locate(k, s)); }
+
+__device__ __forceinline__ void store_probe(const Sink& sink, uint64_t i, const State& s, const u32x4& rec) {
+  if (sink.hash_out) {
+    const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
+    reinterpret_cast<u32x4*>(sink.hash_out)[i] = v;
+  }
+  reinterpret_cast<u32x4*>(sink.out)[i] = rec;
 }
 
 template <int OUT>
@@ -101,11 +131,7 @@ __device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const
   } else if constexpr (OUT == kOutUid) {
     reinterpret_cast<uint64_t*>(sink.out)[i] = uid_parts(s);
   } else {
-    if (sink.hash_out) {
-      u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
-      reinterpret_cast<u32x4*>(sink.hash_out)[i] = v;
-    }
-    reinterpret_cast<u32x4*>(sink.out)[i] = probe_row(sink, s);
+    store_probe(sink, i, s, probe_row(sink, s));
   }
 }
 
@@ -139,19 +165,48 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 #endif
 constexpr uint32_t kF16Block = SHFHB_F16_BLOCK;
 constexpr uint32_t kF16Kpl = SHFHB_F16_KPL;
+#ifndef SHFHB_PROBE_KPL
+#define SHFHB_PROBE_KPL 1  // keys per lane of the fused hash + row pre-probe
+#endif
+template <int OUT>
+constexpr uint32_t kF16KplOf = OUT == kOutProbe ? (uint32_t)SHFHB_PROBE_KPL : kF16Kpl;
 
 template <int OUT>
 __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
                                                        Sink sink) {
-  const uint64_t i0 = (uint64_t)blockIdx.x * (kF16Block * kF16Kpl) + threadIdx.x;
-  u32x4 k[kF16Kpl];
+  constexpr uint32_t kpl = kF16KplOf<OUT>;
+  const uint64_t i0 = (uint64_t)blockIdx.x * (kF16Block * kpl) + threadIdx.x;
+  u32x4 k[kpl];
 #pragma unroll
-  for (uint32_t j = 0; j < kF16Kpl; ++j) {
+  for (uint32_t j = 0; j < kpl; ++j) {
     const uint64_t i = i0 + j * kF16Block;
+    k[j] = u32x4{0u, 0u, 0u, 0u};
     if (i < n) k[j] = __builtin_nontemporal_load(&keys[i]);
   }
+  if constexpr (OUT == kOutProbe) {
+    // every key's tab-map lookup, then every key's row scan, then the stores: no
+    // store sits between two keys' loads, so all their rows are in flight together
+    State s[kpl];
+    ProbeLoc p[kpl];
+    u32x4 rec[kpl];
 #pragma unroll
-  for (uint32_t j = 0; j < kF16Kpl; ++j) {
+    for (uint32_t j = 0; j < kpl; ++j) {
+      s[j] = State{seed, seed};
+      body_block(s[j], pack64(k[j].x, k[j].y), pack64(k[j].z, k[j].w));
+      finish(s[j], 16);
+      p[j] = probe_locate(sink, s[j]);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kpl; ++j) rec[j] = probe_scan(sink, p[j]);
+#pragma unroll
+    for (uint32_t j = 0; j < kpl; ++j) {
+      const uint64_t i = i0 + j * kF16Block;
+      if (i < n) store_probe(sink, i, s[j], rec[j]);
+    }
+    return;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kpl; ++j) {
     const uint64_t i = i0 + j * kF16Block;
     if (i >= n) return;
     State s{seed, seed};
@@ -484,11 +539,12 @@ __device__ __forceinline__ SpanTile<VAR> span_finish(const uint8_t* bytes, uint6
   return ti;
 }
 
-// Fetch the span into registers: piece q of lane l covers bytes q*1024 + 16l.
+// Fetch the span into registers: piece q of thread l covers bytes
+// q * 1024 * W + 16 l (W waves fetch one span together).
 // Raw buffer loads through a descriptor whose range is exactly the span: lanes
 // past its end get 0 without touching memory, so no per-lane predicate, and no
 // load can reach a page the span does not.
-template <int PIECES>
+template <int PIECES, int W = 1>
 __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
@@ -497,19 +553,19 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
       reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
 #pragma unroll
   for (int q = 0; q < PIECES; ++q)
-    if ((uint32_t)q * 1024u < nb)
-      reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
+    if ((uint32_t)q * 1024u * W < nb)
+      reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u * W + lane * 16u, 0, 2 /* nt */);
 }
 
 // Stage the fetched pieces that hold span bytes (lanes past the span's end
 // write nothing: the window may be exactly the span plus its read slack).
-template <int PIECES>
+template <int PIECES, int W = 1>
 __device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[PIECES], uint32_t span16,
                                            uint32_t lane) {
 #pragma unroll
   for (int q = 0; q < PIECES; ++q)
-    if ((uint32_t)q * 1024u < span16 && (uint32_t)q * 1024u + lane * 16u < span16)
-      reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
+    if ((uint32_t)q * 1024u * W < span16 && (uint32_t)q * 1024u * W + lane * 16u < span16)
+      reinterpret_cast<u32x4*>(lds)[64 * W * q + lane] = reg[q];
 }
 
 // The independent k1/k2 mixes (murmurhash3.c:97, :101) of the 16 bytes that
@@ -748,6 +804,93 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
 }
 
 // ---------------------------------------------------------------------------
+// Sorted span kernel (variable lengths; SHFHB_SPAN_SORT_W = W > 1 makes it the
+// span path). W waves per workgroup stage the span of 64 W consecutive keys
+// exactly as k_span stages 64 (W windows of LDS, W times the fetch width), then
+// counting-sort the keys by 16-B block count (an LDS histogram, a scan in wave
+// 0, a rank table) and wave w hashes the keys of rank [64 w, 64 w + 64). A
+// wave's block loop runs as long as its longest key, so grouping similar
+// lengths takes the loop iterations of a workgroup from W times the maximum of
+// 64 random lengths toward the sum of the per-group maxima (U[8,512], W = 2:
+// ~31 + 31 -> ~16 + 31). A span over the window is streamed per wave in rounds.
+// ---------------------------------------------------------------------------
+#ifndef SHFHB_SPAN_SORT_W
+#define SHFHB_SPAN_SORT_W 1
+#endif
+constexpr uint32_t kSortWaves = SHFHB_SPAN_SORT_W;
+constexpr uint32_t kSortBuckets = 64;  // block counts 0..62, and >= 63
+constexpr uint32_t kSortTableBytes = (kSortBuckets + 3u * 64u * kSortWaves) * 4u;
+constexpr uint32_t kSortAlloc = kSortWaves * kSpanAlloc;
+constexpr uint32_t kSortCap = (kSortAlloc - kSpanPad - kSortTableBytes) & ~15u;
+static_assert(kSortWaves * kVrLdsBytes <= kSortAlloc, "the round fallback needs one window per wave");
+static_assert(kSortCap <= kSortWaves * kSpanPiecesMax * 1024u, "the fetch covers the window");
+
+template <int OUT>
+__global__ __launch_bounds__(64 * kSortWaves) void k_span_sorted(const uint8_t* __restrict__ bytes,
+                                                                 const uint64_t* __restrict__ offsets,
+                                                                 uint64_t off_base, uint64_t n, uint32_t seed,
+                                                                 Sink sink) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
+  uint32_t* hist = span_lds + (kSortCap + kSpanPad) / 4u;  // bucket counts, then bucket starts
+  uint32_t* perm = hist + kSortBuckets;                     // rank -> key of the workgroup
+  uint32_t* kpos = perm + 64u * kSortWaves;                 // key -> its first byte in the window
+  uint32_t* klen = kpos + 64u * kSortWaves;                 // key -> its length
+  const uint32_t t = threadIdx.x;
+  const uint64_t k0 = (uint64_t)blockIdx.x * (64u * kSortWaves);
+  const uint32_t kn = (uint32_t)min<uint64_t>(64u * kSortWaves, n - k0);
+  const bool valid = t < kn;
+  uint64_t start = 0;
+  uint32_t len = 0;
+  if (valid) {
+    const uint64_t o0 = offsets[k0 + t], o1 = offsets[k0 + t + 1];
+    start = o0 - off_base;
+    len = (uint32_t)(o1 - o0);
+  }
+  // the workgroup's span: bytes [first, end) relative to `bytes` (uniform)
+  const uint64_t first = offsets[k0] - off_base, end = offsets[k0 + kn] - off_base;
+  const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
+  uint64_t base = 0;
+  uint32_t span16 = 0;
+  if (end > first) {
+    base = (b + first) & ~(uint64_t)15;
+    const uint64_t span = ((b + end + 15) & ~(uint64_t)15) - base;
+    span16 = span > 0xffffffffull ? 0xffffffffu : (uint32_t)span;
+  }
+  if (span16 > kSortCap) {  // uniform: every wave streams its own 64 keys in rounds
+    vround_tile<OUT>(bytes, k0 + t, valid, start, len, seed, sink,
+                     reinterpret_cast<uint8_t*>(span_lds) + (t >> 6) * kVrLdsBytes);
+    return;
+  }
+  if (t < kSortBuckets) hist[t] = 0u;
+  {
+    u32x4 reg[kSpanPiecesMax];
+    span_fetch<kSpanPiecesMax, kSortWaves>(reg, base, span16, t);
+    span_stage<kSpanPiecesMax, kSortWaves>(span_lds, reg, span16, t);
+  }
+  const uint32_t bucket = min(len >> 4, kSortBuckets - 1u);
+  kpos[t] = span16 ? (uint32_t)(b + start - base) : 0u;
+  klen[t] = len;
+  __syncthreads();
+  const uint32_t rank = atomicAdd(&hist[bucket], 1u);
+  __syncthreads();
+  if (t < 64u) {  // exclusive scan of the 64 bucket counts, one per lane of wave 0
+    const uint32_t h = hist[t];
+    uint32_t x = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+      if (t >= (uint32_t)d) x += y;
+    }
+    hist[t] = x - h;
+  }
+  __syncthreads();
+  perm[hist[bucket] + rank] = t;
+  __syncthreads();
+  const uint32_t lk = perm[t];
+  if (lk < kn) store_result<OUT>(sink, k0 + lk, hash_lds(span_lds, kpos[lk], klen[lk], seed));
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // Workgroups of `kernel` that fit on the whole device at once (cached per device).
@@ -815,6 +958,24 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
   }
 }
 
+// W = kSortWaves waves per workgroup, W x 20 KiB of LDS (over 64 KiB needs the
+// function attribute).
+template <int OUT>
+static hipError_t launch_span_sorted(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
+                                     uint32_t seed, const Sink& sink, hipStream_t st) {
+  constexpr uint64_t per = 64u * kSortWaves;
+  const uint64_t groups = (n + per - 1) / per;
+  if (groups > 0x7fffffffull) return hipErrorInvalidValue;
+  if (kSortAlloc > 65536u) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_span_sorted<OUT>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSortAlloc);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_span_sorted<OUT>), dim3((unsigned)groups), dim3((unsigned)per), kSortAlloc, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, sink);
+  return hipGetLastError();
+}
+
 template <int OUT>
 static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
                                  hipStream_t st, int kernel) {
@@ -841,7 +1002,7 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   switch (kernel) {
     case kKernelFixed16:
     {
-      constexpr uint64_t per_block = (uint64_t)kF16Block * kF16Kpl;
+      constexpr uint64_t per_block = (uint64_t)kF16Block * kF16KplOf<OUT>;
       if (key_len != 16 || !al16 || (n + per_block - 1) / per_block > 0x7fffffffull) return hipErrorInvalidValue;
       hipLaunchKernelGGL(k_fixed16<OUT>, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(kF16Block), 0, st,
                          reinterpret_cast<const u32x4*>(keys), n, seed, sink);
@@ -889,6 +1050,7 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
                        offsets, off_base, n, seed, sink);
     return hipGetLastError();
   }
+  if constexpr (kSortWaves > 1) return launch_span_sorted<OUT>(bytes, offsets, off_base, n, seed, sink, st);
   return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st);
 }
 

@@ -21,11 +21,33 @@ constexpr uint64_t kN2 = 0x38495ab5ull;          // murmurhash3.c:103
 constexpr uint64_t kF1 = 0xff51afd7ed558ccdull;  // murmurhash3.c:65
 constexpr uint64_t kF2 = 0xc4ceb9fe1a85ec53ull;  // murmurhash3.c:67
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-
 __device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
+
+#ifndef SHFHB_ASM_MIX
+#define SHFHB_ASM_MIX 0
+#endif
+#if SHFHB_ASM_MIX
+// r is a compile-time constant after inlining: two v_alignbit_b32 (the
+// compiler's own lowering is a 64-bit shift, a 32-bit shift and an or).
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (r < 32)
+    return pack64(__builtin_amdgcn_alignbit(lo, hi, 32 - r), __builtin_amdgcn_alignbit(hi, lo, 32 - r));
+  return pack64(__builtin_amdgcn_alignbit(hi, lo, 64 - r), __builtin_amdgcn_alignbit(lo, hi, 64 - r));
+}
+// x * 5 as one v_lshl_add_u64 (x << 2) + x; the compiler's lowering of a
+// multiply by 5 is two v_mad_u64_u32.
+__device__ __forceinline__ uint64_t mul5(uint64_t x) {
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+#else
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t mul5(uint64_t x) { return x * 5; }
+#endif
 
 __device__ __forceinline__ uint64_t mix_k1(uint64_t k) { return rotl64(k * kC1, 31) * kC2; }
 __device__ __forceinline__ uint64_t mix_k2(uint64_t k) { return rotl64(k * kC2, 33) * kC1; }
@@ -46,7 +68,10 @@ struct State {
 #define SHFHB_CHAIN_DISTRIBUTED 1
 #endif
 __device__ __forceinline__ void chain_block(State& s, uint64_t m1, uint64_t m2) {
-#if SHFHB_CHAIN_DISTRIBUTED
+#if SHFHB_ASM_MIX
+  s.h1 = mul5(rotl64(s.h1 ^ m1, 27) + s.h2) + kN1;
+  s.h2 = mul5(rotl64(s.h2 ^ m2, 31) + s.h1) + kN2;
+#elif SHFHB_CHAIN_DISTRIBUTED
   const uint64_t a1 = rotl64(s.h1 ^ m1, 27) * 5;
   const uint64_t b1 = s.h2 * 5 + kN1;
   const uint64_t a2 = rotl64(s.h2 ^ m2, 31) * 5;

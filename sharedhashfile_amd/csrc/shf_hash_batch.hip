@@ -3,11 +3,12 @@
 // Replaces, for batches, the per-key seam shf_make_hash() (/root/reference/src/shf.c:450-462):
 // same 16 output bytes per key (SHF_HASH layout, shf.private.h:180-185), computed by the
 // kernels in kernels.hip. This file owns: argument checking, per-thread/per-device HIP
-// contexts (streams + staging buffers), the host-memory pipeline (pinned double-buffered
-// chunks, H2D / kernel / D2H overlapped on two streams) and the multi-GPU split.
+// contexts (streams + staging buffers), the host-memory pipeline (pinned chunks, H2D /
+// kernel / D2H overlapped on one stream per chunk in flight) and the multi-GPU split.
 // There is deliberately no CPU path: without a gfx950 device every call fails loudly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -54,8 +55,24 @@ int map_hip(hipError_t e) {
   } while (0)
 
 constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `const int len`
-constexpr size_t kStageBytes = (size_t)64 << 20;   // key bytes per pipeline chunk
-constexpr int kSlots = 2;                          // double buffering
+// Shape of the host-memory pipelines: SHF_HB_STAGE_MB MiB of key bytes per
+// chunk, SHF_HB_SLOTS (2..4) chunks in flight, one stream each. Both are read on
+// every call (tools/host_pipeline_sweep.py, profiles/r1/host_pipeline_sweep.txt).
+constexpr int kMaxSlots = 4;
+constexpr long kDefaultStageMb = 64;
+constexpr int kDefaultSlots = 2;
+
+size_t stage_bytes() {
+  const char* e = getenv("SHF_HB_STAGE_MB");
+  const long mb = e ? strtol(e, nullptr, 10) : 0;
+  return (size_t)(mb >= 1 && mb <= 4096 ? mb : kDefaultStageMb) << 20;
+}
+
+int pipeline_slots() {
+  const char* e = getenv("SHF_HB_SLOTS");
+  const long v = e ? strtol(e, nullptr, 10) : 0;
+  return v >= 2 && v <= kMaxSlots ? (int)v : kDefaultSlots;
+}
 
 shfhb::Sink out_sink(void* out) {
   shfhb::Sink k;
@@ -67,19 +84,20 @@ shfhb::Sink out_sink(void* out) {
 struct DevCtx {
   int dev = -1;
   int status = SHF_HB_OK;
-  hipStream_t st[kSlots] = {nullptr, nullptr};
-  hipEvent_t done[kSlots] = {nullptr, nullptr};
-  uint8_t* h_in[kSlots] = {nullptr, nullptr};
-  uint8_t* d_in[kSlots] = {nullptr, nullptr};
+  hipStream_t st[kMaxSlots] = {};
+  hipEvent_t done[kMaxSlots] = {};
+  uint8_t* h_in[kMaxSlots] = {};
+  uint8_t* d_in[kMaxSlots] = {};
   size_t in_cap = 0;
-  shf_hash128* h_out[kSlots] = {nullptr, nullptr};
-  shf_hash128* d_out[kSlots] = {nullptr, nullptr};
-  uint64_t* h_off[kSlots] = {nullptr, nullptr};
-  uint64_t* d_off[kSlots] = {nullptr, nullptr};
+  shf_hash128* h_out[kMaxSlots] = {};
+  shf_hash128* d_out[kMaxSlots] = {};
+  uint64_t* h_off[kMaxSlots] = {};
+  uint64_t* d_off[kMaxSlots] = {};
   size_t key_cap = 0;  // records in h_out/d_out and offsets (+1) per slot
-  shf_probe* h_probe[kSlots] = {nullptr, nullptr};  // row pre-probe records (allocated on first use)
-  shf_probe* d_probe[kSlots] = {nullptr, nullptr};
+  shf_probe* h_probe[kMaxSlots] = {};  // row pre-probe records (allocated on first use)
+  shf_probe* d_probe[kMaxSlots] = {};
   size_t probe_cap = 0;
+  int n_staged = 0;  // slots whose staging buffers are allocated
 };
 
 thread_local std::map<int, DevCtx*> tls_ctx;
@@ -107,7 +125,7 @@ int current_ctx(DevCtx** out) {
   c->dev = dev;
   c->status = check_arch(dev);
   if (c->status == SHF_HB_OK) {
-    for (int s = 0; s < kSlots && c->status == SHF_HB_OK; ++s) {
+    for (int s = 0; s < kMaxSlots && c->status == SHF_HB_OK; ++s) {
       c->status = map_hip(hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking));
       if (c->status == SHF_HB_OK) c->status = map_hip(hipEventCreateWithFlags(&c->done[s], hipEventDisableTiming));
     }
@@ -118,7 +136,7 @@ int current_ctx(DevCtx** out) {
 }
 
 void free_staging(DevCtx* c) {
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < kMaxSlots; ++s) {
     if (c->h_in[s]) (void)hipHostFree(c->h_in[s]);
     if (c->d_in[s]) (void)hipFree(c->d_in[s]);
     if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
@@ -133,6 +151,7 @@ void free_staging(DevCtx* c) {
     c->h_probe[s] = c->d_probe[s] = nullptr;
   }
   c->in_cap = c->key_cap = c->probe_cap = 0;
+  c->n_staged = 0;
 }
 
 // Release every context of this thread (worker threads of the *_multi calls).
@@ -142,11 +161,11 @@ void release_thread_ctx() {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->dev);
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < kMaxSlots; ++s) {
       if (c->st[s]) (void)hipStreamSynchronize(c->st[s]);
     }
     free_staging(c);
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < kMaxSlots; ++s) {
       if (c->done[s]) (void)hipEventDestroy(c->done[s]);
       if (c->st[s]) (void)hipStreamDestroy(c->st[s]);
     }
@@ -156,12 +175,13 @@ void release_thread_ctx() {
   tls_ctx.clear();
 }
 
-int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys) {
-  if (in_bytes <= c->in_cap && keys <= c->key_cap) return SHF_HB_OK;
-  for (int s = 0; s < kSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
+int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys, int slots) {
+  if (in_bytes <= c->in_cap && keys <= c->key_cap && slots <= c->n_staged) return SHF_HB_OK;
+  for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
   const size_t ib = std::max(in_bytes, c->in_cap), kc = std::max(keys, c->key_cap);
+  const int ns = std::max(slots, c->n_staged);
   free_staging(c);
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < ns; ++s) {
     HB_TRY(hipHostMalloc((void**)&c->h_in[s], ib, hipHostMallocDefault));
     HB_TRY(hipMalloc((void**)&c->d_in[s], ib));
     HB_TRY(hipHostMalloc((void**)&c->h_out[s], kc * sizeof(shf_hash128), hipHostMallocDefault));
@@ -171,20 +191,21 @@ int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys) {
   }
   c->in_cap = ib;
   c->key_cap = kc;
+  c->n_staged = ns;
   return SHF_HB_OK;
 }
 
 // Probe-record staging, key_cap records per slot (after ensure_staging).
 int ensure_probe_staging(DevCtx* c) {
   if (c->probe_cap >= c->key_cap) return SHF_HB_OK;
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < kMaxSlots; ++s) {
     HB_TRY(hipStreamSynchronize(c->st[s]));
     if (c->h_probe[s]) (void)hipHostFree(c->h_probe[s]);
     if (c->d_probe[s]) (void)hipFree(c->d_probe[s]);
     c->h_probe[s] = c->d_probe[s] = nullptr;
   }
   c->probe_cap = 0;
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < c->n_staged; ++s) {
     HB_TRY(hipHostMalloc((void**)&c->h_probe[s], c->key_cap * sizeof(shf_probe), hipHostMallocDefault));
     HB_TRY(hipMalloc((void**)&c->d_probe[s], c->key_cap * sizeof(shf_probe)));
   }
@@ -287,16 +308,17 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  const uint64_t per = key_len ? std::max<uint64_t>(1, kStageBytes / key_len) : (uint64_t)1 << 22;
+  const int ns = pipeline_slots();
+  const uint64_t per = key_len ? std::max<uint64_t>(1, stage_bytes() / key_len) : (uint64_t)1 << 22;
   const uint64_t chunk = std::min<uint64_t>(per, n);
-  if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk))) return rc;
+  if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk, ns))) return rc;
   if (job.probe && (rc = ensure_probe_staging(c))) return rc;
   const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
              probe_pinned = is_host_pinned(job.probe);
-  Pending pend[kSlots];
+  Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += chunk, ++idx) {
-    const int s = (int)(idx % kSlots);
+    const int s = (int)(idx % ns);
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
     const uint64_t cnt = std::min(chunk, n - i0);
     const size_t nb = (size_t)cnt * key_len;
@@ -309,7 +331,7 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto));
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
   }
-  for (int s = 0; s < kSlots; ++s)
+  for (int s = 0; s < ns; ++s)
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
   return SHF_HB_OK;
 }
@@ -330,16 +352,18 @@ int var_kernel_for(uint64_t bytes, uint64_t keys) {
   return shfhb::kKernelRound;
 }
 
-// Host-memory variable-length pipeline: chunks of whole keys up to kStageBytes
+// Host-memory variable-length pipeline: chunks of whole keys up to stage_bytes()
 // of key bytes (a single larger key gets a chunk of its own).
 int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  const uint64_t max_keys = std::min<uint64_t>(n, (uint64_t)1 << 22);
+  const int ns = pipeline_slots();
+  const uint64_t stage = stage_bytes();
+  const uint64_t max_keys = std::min<uint64_t>(n, std::max<uint64_t>(stage / 16, (uint64_t)1 << 16));
   const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
              hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
-  Pending pend[kSlots];
+  Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
     // extend the chunk while it fits the byte budget and key budget
@@ -347,10 +371,10 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     const uint64_t base = offsets[i0];
     {
       uint64_t lo = i1, hi = std::min(n, i0 + max_keys);
-      // largest i1 in [i0+1, hi] with offsets[i1] - base <= kStageBytes (offsets monotone)
+      // largest i1 in [i0+1, hi] with offsets[i1] - base <= stage (offsets monotone)
       while (lo < hi) {
         const uint64_t mid = lo + (hi - lo + 1) / 2;
-        if (offsets[mid] - base <= kStageBytes) lo = mid;
+        if (offsets[mid] - base <= stage) lo = mid;
         else hi = mid - 1;
       }
       i1 = lo;
@@ -358,14 +382,14 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     const uint64_t cnt = i1 - i0;
     const size_t nb = (size_t)(offsets[i1] - base);
     const size_t need_keys = (size_t)std::max<uint64_t>(cnt, max_keys);
-    if (nb > c->in_cap || need_keys > c->key_cap) {
+    if (nb > c->in_cap || need_keys > c->key_cap || c->n_staged < ns) {
       // growing the staging buffers frees them: collect every chunk in flight first
-      for (int s = 0; s < kSlots; ++s)
+      for (int s = 0; s < ns; ++s)
         if ((rc = drain_slot(c, s, pend[s]))) return rc;
-      if ((rc = ensure_staging(c, std::max(nb, (size_t)1), need_keys))) return rc;
+      if ((rc = ensure_staging(c, std::max(nb, (size_t)1), need_keys, ns))) return rc;
     }
     if (job.probe && (rc = ensure_probe_staging(c))) return rc;
-    const int s = (int)(idx % kSlots);
+    const int s = (int)(idx % ns);
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
     if (nb && !in_pinned) par_memcpy(c->h_in[s], bytes + base, nb);
     const uint64_t* off_src = offsets + i0;
@@ -383,7 +407,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
     i0 = i1;
   }
-  for (int s = 0; s < kSlots; ++s)
+  for (int s = 0; s < ns; ++s)
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
   return SHF_HB_OK;
 }
@@ -396,7 +420,7 @@ int drain_on_error(int rc) {
   const int hip = tls_last_hip;
   DevCtx* c = nullptr;
   if (current_ctx(&c) == SHF_HB_OK)
-    for (int s = 0; s < kSlots; ++s) (void)hipStreamSynchronize(c->st[s]);
+    for (int s = 0; s < kMaxSlots; ++s) (void)hipStreamSynchronize(c->st[s]);
   (void)hipGetLastError();
   tls_last_hip = hip;
   return rc;

@@ -187,6 +187,33 @@ def test_var_span_edges(hb, dev, oracle):
             assert np.array_equal(got, want), (lens[:3], k)
 
 
+def test_var_sort_groups(hb, dev, oracle):
+    """Length patterns for a span path that hashes a workgroup's keys in
+    block-count order (SHFHB_SPAN_SORT_W > 1): one bucket for all keys, rising
+    and falling lengths, keys past the last bucket (>= 63 blocks), 128-key
+    spans just under / over a two-wave window, a partial last group, empty keys
+    mixed in."""
+    rng = np.random.default_rng(41)
+    cases = [
+        np.full(1000, 100, np.int64),
+        np.arange(0, 1024, dtype=np.int64) % 700,
+        np.arange(1024, 0, -1, dtype=np.int64) % 700,
+        rng.choice([0, 1, 15, 16, 17, 1007, 1008, 1009, 2000], size=3000),
+        np.full(128, 305, np.int64),
+        np.full(128, 306, np.int64),
+        np.full(256, 152, np.int64),
+        np.concatenate([rng.integers(0, 600, 500), np.zeros(77, np.int64)]),
+    ]
+    for lens in cases:
+        off = np.zeros(lens.size + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        data = rng.integers(0, 256, size=max(int(off[-1]), 1), dtype=np.uint8)
+        want = oracle.hash_var(data, off)
+        for k in VAR_KERNELS:
+            got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k))
+            assert np.array_equal(got, want), (lens[:3], k)
+
+
 def test_var_many_tiles(hb, dev, oracle):
     """A large batch (23k tiles) with a few tiles over the LDS window in between."""
     rng = np.random.default_rng(23)
@@ -353,6 +380,25 @@ def test_host_var_kernel_by_mean_length(hb, dev, oracle, lo, hi):
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens)
     data = np.frombuffer(splitmix_bytes(int(off[-1]) + 3, lo + 1), dtype=np.uint8)[3:]
+    assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
+
+
+@pytest.mark.parametrize("stage_mb,slots", [(1, 2), (1, 4), (3, 3), (64, 2)])
+def test_host_pipeline_shapes(hb, dev, oracle, monkeypatch, stage_mb, slots):
+    """SHF_HB_STAGE_MB / SHF_HB_SLOTS change only how a host batch is chunked
+    and overlapped (many chunks, a key larger than a chunk)."""
+    monkeypatch.setenv("SHF_HB_STAGE_MB", str(stage_mb))
+    monkeypatch.setenv("SHF_HB_SLOTS", str(slots))
+    n = 600_000
+    flat = np.frombuffer(splitmix_bytes(n * 16, 31), dtype=np.uint8)
+    assert np.array_equal(hb.hash_fixed_host(flat, 16), oracle.hash_fixed(flat, 16, threads=8))
+    rng = np.random.default_rng(stage_mb * 10 + slots)
+    m = 20_000
+    lens = rng.integers(0, 700, size=m)
+    lens[5] = 3 << 20
+    off = np.zeros(m + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
     assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
 
 

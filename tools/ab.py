@@ -49,7 +49,6 @@ def main():
     p.add_argument("--var-lo", type=int, default=8, help="var workload: key lengths U[var-lo, var-hi]")
     p.add_argument("--var-hi", type=int, default=512)
     p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
-    p.add_argument("--graph", action="store_true", help="time `reps` launches captured in one HIP graph")
     p.add_argument("--prebuild", default="", help="build every name=-Dflags variant into this dir and exit")
     a = p.parse_args()
     if a.prebuild:
@@ -64,7 +63,7 @@ def main():
     import sharedhashfile_amd as hb
     from sharedhashfile_amd.keygen import device_random_bytes
 
-    def cs():  # the current stream's handle (a capture stream inside torch.cuda.graph)
+    def cs():  # the current stream's handle
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     outdir = tempfile.mkdtemp(prefix="shfhb_ab_")
@@ -124,26 +123,14 @@ def main():
         outs["copy_ref"] = None
         call_orig = call
         call = lambda lib, out: (dst_c.copy_(src_c), 0)[1] if lib is None else call_orig(lib, out)
-    graphs = {}
-    if a.graph:
-        for k, lib in libs.items():
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(a.reps):
-                    call(lib, outs[k])
-            graphs[k] = g
-        torch.cuda.synchronize()
     times = {k: [] for k in libs}
     for r in range(a.rounds):
         for k, lib in libs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record()
-            if k in graphs:
-                graphs[k].replay()
-            else:
-                for _ in range(a.reps):
-                    call(lib, outs[k])
+            for _ in range(a.reps):
+                call(lib, outs[k])
             e1.record()
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.reps)
