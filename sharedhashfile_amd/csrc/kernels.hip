@@ -17,8 +17,6 @@
 //   k_span      variable-length keys and most other fixed lengths: a wave owns a
 //               tile of 64 consecutive keys = one contiguous span, fetched with
 //               1-KiB raw buffer loads, staged in LDS, hashed lane-per-key.
-//   k_span_sorted  (SHFHB_SPAN_SORT_W > 1) the variable-length span path with W
-//               waves per workgroup hashing its 64 W keys in block-count order.
 //   k_vround    variable-length keys streamed 128 B per key per round through
 //               144-B LDS windows (short / very long keys, k_span's overflow).
 //   k_generic   any length, fixed or variable (offset array): one lane per key,
@@ -166,7 +164,7 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 constexpr uint32_t kF16Block = SHFHB_F16_BLOCK;
 constexpr uint32_t kF16Kpl = SHFHB_F16_KPL;
 #ifndef SHFHB_PROBE_KPL
-#define SHFHB_PROBE_KPL 1  // keys per lane of the fused hash + row pre-probe
+#define SHFHB_PROBE_KPL 1  // keys per lane of the fused hash + row pre-probe (2 and 4 measured ~2 % slower)
 #endif
 template <int OUT>
 constexpr uint32_t kF16KplOf = OUT == kOutProbe ? (uint32_t)SHFHB_PROBE_KPL : kF16Kpl;
@@ -539,12 +537,11 @@ __device__ __forceinline__ SpanTile<VAR> span_finish(const uint8_t* bytes, uint6
   return ti;
 }
 
-// Fetch the span into registers: piece q of thread l covers bytes
-// q * 1024 * W + 16 l (W waves fetch one span together).
+// Fetch the span into registers: piece q of lane l covers bytes q*1024 + 16l.
 // Raw buffer loads through a descriptor whose range is exactly the span: lanes
 // past its end get 0 without touching memory, so no per-lane predicate, and no
 // load can reach a page the span does not.
-template <int PIECES, int W = 1>
+template <int PIECES>
 __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
@@ -553,19 +550,19 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
       reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
 #pragma unroll
   for (int q = 0; q < PIECES; ++q)
-    if ((uint32_t)q * 1024u * W < nb)
-      reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u * W + lane * 16u, 0, 2 /* nt */);
+    if ((uint32_t)q * 1024u < nb)
+      reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
 // Stage the fetched pieces that hold span bytes (lanes past the span's end
 // write nothing: the window may be exactly the span plus its read slack).
-template <int PIECES, int W = 1>
+template <int PIECES>
 __device__ __forceinline__ void span_stage(uint32_t* lds, const u32x4 (&reg)[PIECES], uint32_t span16,
                                            uint32_t lane) {
 #pragma unroll
   for (int q = 0; q < PIECES; ++q)
-    if ((uint32_t)q * 1024u * W < span16 && (uint32_t)q * 1024u * W + lane * 16u < span16)
-      reinterpret_cast<u32x4*>(lds)[64 * W * q + lane] = reg[q];
+    if ((uint32_t)q * 1024u < span16 && (uint32_t)q * 1024u + lane * 16u < span16)
+      reinterpret_cast<u32x4*>(lds)[64 * q + lane] = reg[q];
 }
 
 // The independent k1/k2 mixes (murmurhash3.c:97, :101) of the 16 bytes that
@@ -804,93 +801,6 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
 }
 
 // ---------------------------------------------------------------------------
-// Sorted span kernel (variable lengths; SHFHB_SPAN_SORT_W = W > 1 makes it the
-// span path). W waves per workgroup stage the span of 64 W consecutive keys
-// exactly as k_span stages 64 (W windows of LDS, W times the fetch width), then
-// counting-sort the keys by 16-B block count (an LDS histogram, a scan in wave
-// 0, a rank table) and wave w hashes the keys of rank [64 w, 64 w + 64). A
-// wave's block loop runs as long as its longest key, so grouping similar
-// lengths takes the loop iterations of a workgroup from W times the maximum of
-// 64 random lengths toward the sum of the per-group maxima (U[8,512], W = 2:
-// ~31 + 31 -> ~16 + 31). A span over the window is streamed per wave in rounds.
-// ---------------------------------------------------------------------------
-#ifndef SHFHB_SPAN_SORT_W
-#define SHFHB_SPAN_SORT_W 1
-#endif
-constexpr uint32_t kSortWaves = SHFHB_SPAN_SORT_W;
-constexpr uint32_t kSortBuckets = 64;  // block counts 0..62, and >= 63
-constexpr uint32_t kSortTableBytes = (kSortBuckets + 3u * 64u * kSortWaves) * 4u;
-constexpr uint32_t kSortAlloc = kSortWaves * kSpanAlloc;
-constexpr uint32_t kSortCap = (kSortAlloc - kSpanPad - kSortTableBytes) & ~15u;
-static_assert(kSortWaves * kVrLdsBytes <= kSortAlloc, "the round fallback needs one window per wave");
-static_assert(kSortCap <= kSortWaves * kSpanPiecesMax * 1024u, "the fetch covers the window");
-
-template <int OUT>
-__global__ __launch_bounds__(64 * kSortWaves) void k_span_sorted(const uint8_t* __restrict__ bytes,
-                                                                 const uint64_t* __restrict__ offsets,
-                                                                 uint64_t off_base, uint64_t n, uint32_t seed,
-                                                                 Sink sink) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  uint32_t* hist = span_lds + (kSortCap + kSpanPad) / 4u;  // bucket counts, then bucket starts
-  uint32_t* perm = hist + kSortBuckets;                     // rank -> key of the workgroup
-  uint32_t* kpos = perm + 64u * kSortWaves;                 // key -> its first byte in the window
-  uint32_t* klen = kpos + 64u * kSortWaves;                 // key -> its length
-  const uint32_t t = threadIdx.x;
-  const uint64_t k0 = (uint64_t)blockIdx.x * (64u * kSortWaves);
-  const uint32_t kn = (uint32_t)min<uint64_t>(64u * kSortWaves, n - k0);
-  const bool valid = t < kn;
-  uint64_t start = 0;
-  uint32_t len = 0;
-  if (valid) {
-    const uint64_t o0 = offsets[k0 + t], o1 = offsets[k0 + t + 1];
-    start = o0 - off_base;
-    len = (uint32_t)(o1 - o0);
-  }
-  // the workgroup's span: bytes [first, end) relative to `bytes` (uniform)
-  const uint64_t first = offsets[k0] - off_base, end = offsets[k0 + kn] - off_base;
-  const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
-  uint64_t base = 0;
-  uint32_t span16 = 0;
-  if (end > first) {
-    base = (b + first) & ~(uint64_t)15;
-    const uint64_t span = ((b + end + 15) & ~(uint64_t)15) - base;
-    span16 = span > 0xffffffffull ? 0xffffffffu : (uint32_t)span;
-  }
-  if (span16 > kSortCap) {  // uniform: every wave streams its own 64 keys in rounds
-    vround_tile<OUT>(bytes, k0 + t, valid, start, len, seed, sink,
-                     reinterpret_cast<uint8_t*>(span_lds) + (t >> 6) * kVrLdsBytes);
-    return;
-  }
-  if (t < kSortBuckets) hist[t] = 0u;
-  {
-    u32x4 reg[kSpanPiecesMax];
-    span_fetch<kSpanPiecesMax, kSortWaves>(reg, base, span16, t);
-    span_stage<kSpanPiecesMax, kSortWaves>(span_lds, reg, span16, t);
-  }
-  const uint32_t bucket = min(len >> 4, kSortBuckets - 1u);
-  kpos[t] = span16 ? (uint32_t)(b + start - base) : 0u;
-  klen[t] = len;
-  __syncthreads();
-  const uint32_t rank = atomicAdd(&hist[bucket], 1u);
-  __syncthreads();
-  if (t < 64u) {  // exclusive scan of the 64 bucket counts, one per lane of wave 0
-    const uint32_t h = hist[t];
-    uint32_t x = h;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-      if (t >= (uint32_t)d) x += y;
-    }
-    hist[t] = x - h;
-  }
-  __syncthreads();
-  perm[hist[bucket] + rank] = t;
-  __syncthreads();
-  const uint32_t lk = perm[t];
-  if (lk < kn) store_result<OUT>(sink, k0 + lk, hash_lds(span_lds, kpos[lk], klen[lk], seed));
-}
-
-// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // Workgroups of `kernel` that fit on the whole device at once (cached per device).
@@ -956,24 +866,6 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
     if (span <= 4096) return launch_span_p<OUT, VAR, 4>(bytes, offsets, off_base, key_len, n, seed, sink, st, lds);
     return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, key_len, n, seed, sink, st, lds);
   }
-}
-
-// W = kSortWaves waves per workgroup, W x 20 KiB of LDS (over 64 KiB needs the
-// function attribute).
-template <int OUT>
-static hipError_t launch_span_sorted(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                                     uint32_t seed, const Sink& sink, hipStream_t st) {
-  constexpr uint64_t per = 64u * kSortWaves;
-  const uint64_t groups = (n + per - 1) / per;
-  if (groups > 0x7fffffffull) return hipErrorInvalidValue;
-  if (kSortAlloc > 65536u) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_span_sorted<OUT>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSortAlloc);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL((k_span_sorted<OUT>), dim3((unsigned)groups), dim3((unsigned)per), kSortAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, sink);
-  return hipGetLastError();
 }
 
 template <int OUT>
@@ -1050,7 +942,6 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
                        offsets, off_base, n, seed, sink);
     return hipGetLastError();
   }
-  if constexpr (kSortWaves > 1) return launch_span_sorted<OUT>(bytes, offsets, off_base, n, seed, sink, st);
   return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st);
 }
 

@@ -25,8 +25,12 @@ __device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// Rotates as two v_alignbit_b32 and `x * 5` as one v_lshl_add_u64, with the
+// h1/h2 chain left undistributed (two *5 per block instead of four): k_span
+// +7.8 %, k_vround +5.2 % on U[8,512] keys, fixed-length kernels unchanged
+// (HBM-bound) -- profiles/r1/ab_asm/. 0 keeps the compiler's own lowering.
 #ifndef SHFHB_ASM_MIX
-#define SHFHB_ASM_MIX 0
+#define SHFHB_ASM_MIX 1
 #endif
 #if SHFHB_ASM_MIX
 // r is a compile-time constant after inlining: two v_alignbit_b32 (the

@@ -187,12 +187,11 @@ def test_var_span_edges(hb, dev, oracle):
             assert np.array_equal(got, want), (lens[:3], k)
 
 
-def test_var_sort_groups(hb, dev, oracle):
-    """Length patterns for a span path that hashes a workgroup's keys in
-    block-count order (SHFHB_SPAN_SORT_W > 1): one bucket for all keys, rising
-    and falling lengths, keys past the last bucket (>= 63 blocks), 128-key
-    spans just under / over a two-wave window, a partial last group, empty keys
-    mixed in."""
+def test_var_length_patterns(hb, dev, oracle):
+    """Length patterns across tiles: all keys equal, rising and falling
+    lengths, a mix of tiny and ~1-2 KB keys (tiles over the span window next to
+    staged ones), 128- and 256-key batches of equal keys (whole tiles near the
+    window size), a ragged batch ending in empty keys."""
     rng = np.random.default_rng(41)
     cases = [
         np.full(1000, 100, np.int64),
