@@ -168,7 +168,7 @@ def make_workloads(args, dev, rank, world=1):
         del lens
         wl.append(Workload("var", n, total / n + 8 + 16,
                            lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]:
-                           hb.hash_var(d, o, out=out, kernel=vk),
+                           hb.hash_var(d, o, out=out, kernel=vk, key_bytes=total),
                            {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding

@@ -104,6 +104,16 @@ SHF_HB_API int shf_hash_batch_var(const void *bytes, const uint64_t *offsets, ui
 SHF_HB_API int shf_hash_batch_var_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n, uint32_t seed,
                              shf_hash128 *d_out, void *hip_stream);
 
+/* As shf_hash_batch_var_async, for a caller that knows the batch's packed byte
+ * count key_bytes = offsets[n] - offsets[0] (whoever packed the keys does). The
+ * mean key length sizes the LDS window of each 64-key span, so batches of
+ * short keys keep more spans in flight per CU (U[8,128] B keys: 5.1 vs
+ * 3.4 TB/s). A wrong key_bytes changes the speed, never the results. The
+ * host-memory calls do this by themselves. (An extension: the reference hashes
+ * one key at a time and has no such parameter.) */
+SHF_HB_API int shf_hash_batch_var_sized_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                                   uint64_t key_bytes, uint32_t seed, shf_hash128 *d_out, void *hip_stream);
+
 /* ---- UID parts instead of the 16-byte hash (8 B per key, see above) ------- */
 
 SHF_HB_API int shf_uid_parts_batch_fixed_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
@@ -133,6 +143,9 @@ SHF_HB_API int shf_hash_batch_fixed_kernel_async(const void *d_keys, uint32_t ke
 /* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_ROUND or SHF_HB_KERNEL_GENERIC */
 SHF_HB_API int shf_hash_batch_var_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                     uint32_t seed, shf_hash128 *d_out, int kernel, void *hip_stream);
+SHF_HB_API int shf_hash_batch_var_sized_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                                          uint64_t key_bytes, uint32_t seed, shf_hash128 *d_out, int kernel,
+                                          void *hip_stream);
 
 /* ---- row pre-probe ----------------------------------------
  *

@@ -76,6 +76,8 @@ _SIGS = {
     "shf_hash_batch_var_multi": [_VP, _VP, _U64, _U32, _VP, _INT],
     "shf_hash_batch_fixed_kernel_async": [_VP, _U32, _U64, _U32, _VP, _INT, _VP],
     "shf_hash_batch_var_kernel_async": [_VP, _VP, _U64, _U32, _VP, _INT, _VP],
+    "shf_hash_batch_var_sized_async": [_VP, _VP, _U64, _U64, _U32, _VP, _VP],
+    "shf_hash_batch_var_sized_kernel_async": [_VP, _VP, _U64, _U64, _U32, _VP, _INT, _VP],
     "shf_row_index_create": [_U64, ctypes.POINTER(_VP)],
     "shf_row_index_destroy": [_VP],
     "shf_row_index_set_tabs": [_VP, _VP],
@@ -174,10 +176,12 @@ def hash_fixed(keys, key_len=None, seed=SEED, out=None, stream=None, kernel=KERN
     return out
 
 
-def hash_var(data, offsets, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO):
+def hash_var(data, offsets, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO, key_bytes=None):
     """Hash n variable-length keys on the GPU: key i = data[offsets[i]:offsets[i+1]].
 
     data: uint8 CUDA tensor; offsets: int64 CUDA tensor of n + 1 entries.
+    key_bytes: offsets[n] - offsets[0] if known (sizes the span kernel's LDS
+    window: shf_hash_batch_var_sized_kernel_async); None = unknown.
     """
     import torch
 
@@ -185,10 +189,16 @@ def hash_var(data, offsets, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO
     n = offsets.numel() - 1
     if out is None:
         out = torch.empty((max(n, 0), 2), dtype=torch.int64, device=data.device)
-    rc = load().shf_hash_batch_var_kernel_async(
-        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
+    if key_bytes is None:
+        rc = load().shf_hash_batch_var_kernel_async(
+            ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
+            ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
+        _check(rc, "shf_hash_batch_var_kernel_async")
+        return out
+    rc = load().shf_hash_batch_var_sized_kernel_async(
+        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), int(key_bytes), seed,
         ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
-    _check(rc, "shf_hash_batch_var_kernel_async")
+    _check(rc, "shf_hash_batch_var_sized_kernel_async")
     return out
 
 

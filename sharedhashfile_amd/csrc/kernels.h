@@ -33,8 +33,11 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
                         int out_mode, hipStream_t st, int kernel);
 
 // Key i = bytes[offsets[i] - off_base, offsets[i+1] - off_base); offsets on device.
+// key_bytes: offsets[n] - offsets[0] when the caller knows it (sizes the span
+// kernel's LDS window; 0 = unknown). It never changes results.
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
-                      const Sink& sink, int out_mode, hipStream_t st, int kernel = kKernelAuto);
+                      const Sink& sink, int out_mode, hipStream_t st, int kernel = kKernelAuto,
+                      uint64_t key_bytes = 0);
 
 // Row pre-probe of precomputed hashes (n x 16 B on device) into sink.out.
 hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st);

@@ -464,7 +464,7 @@ __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __res
 // LDS per workgroup: [0, span) the staged span, then kSpanPad bytes of read
 // slack. Variable-length launches take the full window; fixed-length launches
 // only what one tile's span needs, so more tiles fit a CU.
-constexpr uint32_t kSpanAlloc = 20u * 1024u;                    // 8 workgroups per CU
+constexpr uint32_t kSpanAlloc = 20u * 1024u;                    // 8 workgroups per CU; the most a window takes
 constexpr uint32_t kSpanPad = 64;
 constexpr uint32_t kSpanCap = kSpanAlloc - kSpanPad;            // 20416 B
 constexpr int kSpanPiecesMax = (kSpanCap + 1023u) / 1024u;      // 20
@@ -852,13 +852,35 @@ static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint
   return hipGetLastError();
 }
 
+// LDS window per 64-key tile of a variable-length batch. Unknown byte count:
+// 20 KiB (8 tiles per CU; config D's U[8,512] spans average 16.6 KB). Known
+// (key_bytes = offsets[n] - offsets[0]): the tile's expected span, 64 x the
+// mean key length, plus a tenth and 512 B, between 10 KiB (what the round
+// fallback of an overflowing tile needs) and 20 KiB. Smaller windows keep more
+// tiles in flight per CU: at 10 vs 20 KiB U[8,128] keys run at 5.11 vs 3.38
+// TB/s, U[8,256] at 5.66 vs 4.27 (profiles/r1/ab_window/).
+constexpr uint32_t kSpanMinAlloc = 10u * 1024u;
+static_assert(kSpanMinAlloc >= kVrLdsBytes, "an overflowing tile is streamed through its window");
+
+static uint32_t span_window(uint64_t n, uint64_t key_bytes) {
+  if (key_bytes == 0 || n == 0) return kSpanAlloc;
+  const double span = 64.0 * (double)key_bytes / (double)n;
+  const double w = span * 1.1 + 512.0 + kSpanPad;
+  if (w >= (double)kSpanAlloc) return kSpanAlloc;
+  const uint32_t lds = ((uint32_t)w + 255u) & ~255u;
+  return lds < kSpanMinAlloc ? kSpanMinAlloc : lds;
+}
+
 // Fixed lengths: a tile's span is at most 64 * key_len + 15 bytes, so the LDS
 // request (and the fetch) is sized to that; variable lengths use the window.
 template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
-                              uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st) {
+                              uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0) {
   if constexpr (VAR) {
-    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, kSpanAlloc);
+    const uint32_t lds = span_window(n, key_bytes);
+    if (lds - kSpanPad <= 10u * 1024u)
+      return launch_span_p<OUT, VAR, 10>(bytes, offsets, off_base, 0, n, seed, sink, st, lds);
+    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, lds);
   } else {
     const uint32_t span = ((uint32_t)key_len * 64u + 15u + 15u) & ~15u;
     const uint32_t lds = (span + kSpanPad + 255u) & ~255u;
@@ -929,7 +951,12 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
 
 template <int OUT>
 static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                               uint32_t seed, const Sink& sink, hipStream_t st, int kernel) {
+                               uint32_t seed, const Sink& sink, hipStream_t st, int kernel, uint64_t key_bytes) {
+  // AUTO with a known byte count: the span kernel with a sized window up to a
+  // mean key length of 300 B; beyond, 64-key spans overflow even 20 KiB and the
+  // round kernel streams them (profiles/r1/sweep_var: U[8,2048] round 3797,
+  // span 3247 GB/s).
+  if (kernel == kKernelAuto && key_bytes != 0 && key_bytes / n > 300) kernel = kKernelRound;
   if (kernel == kKernelGeneric) {
     hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, sink);
@@ -942,7 +969,7 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
                        offsets, off_base, n, seed, sink);
     return hipGetLastError();
   }
-  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st);
+  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st, key_bytes);
 }
 
 hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
@@ -959,15 +986,15 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
 }
 
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
-                      const Sink& sink, int out_mode, hipStream_t st, int kernel) {
+                      const Sink& sink, int out_mode, hipStream_t st, int kernel, uint64_t key_bytes) {
   if (n == 0) return hipSuccess;
   switch (out_mode) {
     case kOutHash:
-      return launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, sink, st, kernel);
+      return launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     case kOutUid:
-      return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel);
+      return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     default:
-      return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel);
+      return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
   }
 }
 

@@ -336,22 +336,6 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   return SHF_HB_OK;
 }
 
-// The host path knows each chunk's key bytes, so it picks the variable-length
-// kernel by mean key length (tools/sweep_var.sh, profiles/r1/sweep_var/, GB/s):
-//   mean  36 B (U[8,64]):   generic 4003, round 2804, span 2516
-//   mean  68 B (U[8,128]):  round 3769, generic 3501, span 3206
-//   mean 132 B (U[8,256]):  round 3807 = span 3805
-//   mean 260 B (U[8,512]):  span 4148, round 3776
-//   mean 1028 B (U[8,2048]): round 3797, span 3247 (64-key spans overflow its window)
-// Device-resident calls cannot see the lengths and use AUTO (span).
-int var_kernel_for(uint64_t bytes, uint64_t keys) {
-  const uint64_t mean = keys ? bytes / keys : 0;
-  if (mean < 48) return shfhb::kKernelGeneric;
-  if (mean < 128) return shfhb::kKernelRound;
-  if (mean <= 300) return shfhb::kKernelSpan;
-  return shfhb::kKernelRound;
-}
-
 // Host-memory variable-length pipeline: chunks of whole keys up to stage_bytes()
 // of key bytes (a single larger key gets a chunk of its own).
 int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job) {
@@ -403,7 +387,8 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     shfhb::Sink k;
     int mode = 0;
     job_sink(c, s, job, &k, &mode);
-    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, k, mode, c->st[s], var_kernel_for(nb, cnt)));
+    // the chunk's byte count sizes the span kernel's window (kernels.hip span_window)
+    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto, nb));
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
     i0 = i1;
   }
@@ -459,12 +444,12 @@ int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, 
 }
 
 int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const shfhb::Sink& sink,
-               int out_mode, hipStream_t st, bool sync, int kernel = shfhb::kKernelAuto) {
+               int out_mode, hipStream_t st, bool sync, int kernel = shfhb::kKernelAuto, uint64_t key_bytes = 0) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
   if (sync) st = c->st[0];
-  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, sink, out_mode, st, kernel));
+  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, sink, out_mode, st, kernel, key_bytes));
   if (sync) HB_TRY(hipStreamSynchronize(st));
   return SHF_HB_OK;
 }
@@ -602,6 +587,26 @@ int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offse
       kernel != SHF_HB_KERNEL_ROUND)
     return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
+}
+
+int shf_hash_batch_var_sized_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint64_t key_bytes,
+                                   uint32_t seed, shf_hash128* d_out, void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
+  return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false,
+                    shfhb::kKernelAuto, key_bytes);
+}
+
+int shf_hash_batch_var_sized_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                                          uint64_t key_bytes, uint32_t seed, shf_hash128* d_out, int kernel,
+                                          void* hip_stream) {
+  if (n == 0) return SHF_HB_OK;
+  if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
+  if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC &&
+      kernel != SHF_HB_KERNEL_ROUND)
+    return SHF_HB_ERR_ARG;
+  return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false,
+                    kernel, key_bytes);
 }
 
 int shf_uid_parts_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,

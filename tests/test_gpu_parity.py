@@ -213,6 +213,31 @@ def test_var_length_patterns(hb, dev, oracle):
             assert np.array_equal(got, want), (lens[:3], k)
 
 
+@pytest.mark.parametrize("lo,hi", [(0, 40), (8, 128), (64, 192), (8, 256), (8, 512), (250, 330), (8, 2048)])
+def test_var_sized_window(hb, dev, oracle, lo, hi):
+    """shf_hash_batch_var_sized_*: the batch's byte count sizes the LDS window
+    (10-20 KiB); the right count, a far too small one (every tile overflows
+    into the round path) and a far too large one give the same hashes."""
+    rng = np.random.default_rng(lo * 7 + hi)
+    n = 30_000
+    lens = rng.integers(lo, hi + 1, size=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]) + 5, lo + hi), dtype=np.uint8)[5:]
+    want = oracle.hash_var(data, off)
+    d_data, d_o = d_u8(data, dev), d_off(off, dev)
+    total = int(off[-1])
+    for kb in (total, 1, total * 50):
+        for k in VAR_KERNELS:
+            got = u64(hb.hash_var(d_data, d_o, kernel=k, key_bytes=kb))
+            assert np.array_equal(got, want), (kb, k)
+    lib = hb.load()
+    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    assert lib.shf_hash_batch_var_sized_async(d_data.data_ptr(), d_o.data_ptr(), n, total, 12345, out.data_ptr(),
+                                              None) == 0
+    assert np.array_equal(u64(out), want)
+
+
 def test_var_many_tiles(hb, dev, oracle):
     """A large batch (23k tiles) with a few tiles over the LDS window in between."""
     rng = np.random.default_rng(23)
@@ -372,7 +397,8 @@ def test_host_var_multi_chunk(hb, dev, oracle):
 
 @pytest.mark.parametrize("lo,hi", [(0, 40), (8, 128), (200, 400), (300, 3000)])
 def test_host_var_kernel_by_mean_length(hb, dev, oracle, lo, hi):
-    """The host path picks generic / round / span / round by mean key length."""
+    """The host path sizes the span kernel's window by each chunk's mean key
+    length, and takes the round kernel past a mean of 300 B."""
     rng = np.random.default_rng(lo + hi)
     n = 40_000
     lens = rng.integers(lo, hi + 1, size=n)

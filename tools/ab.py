@@ -49,6 +49,7 @@ def main():
     p.add_argument("--var-lo", type=int, default=8, help="var workload: key lengths U[var-lo, var-hi]")
     p.add_argument("--var-hi", type=int, default=512)
     p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
+    p.add_argument("--sized", action="store_true", help="var: pass the batch byte count (sized-window API)")
     p.add_argument("--prebuild", default="", help="build every name=-Dflags variant into this dir and exit")
     a = p.parse_args()
     if a.prebuild:
@@ -105,8 +106,13 @@ def main():
         torch.cumsum(lens, 0, out=off[1:])
         data = device_random_bytes(int(off[-1].item()), 2, dev)
         per_key = float(off[-1].item()) / n + 24
-        call = lambda lib, out: lib.shf_hash_batch_var_kernel_async(data.data_ptr(), off.data_ptr(), n, 12345,
-                                                                     out.data_ptr(), a.kernel, cs())
+        total = int(off[-1].item())
+        if a.sized:
+            call = lambda lib, out: lib.shf_hash_batch_var_sized_kernel_async(data.data_ptr(), off.data_ptr(), n, total,
+                                                                               12345, out.data_ptr(), a.kernel, cs())
+        else:
+            call = lambda lib, out: lib.shf_hash_batch_var_kernel_async(data.data_ptr(), off.data_ptr(), n, 12345,
+                                                                         out.data_ptr(), a.kernel, cs())
     outs = {k: torch.empty(out_shape, dtype=torch.int64 if out_shape[1] == 2 else torch.int32, device=dev)
             for k in libs}
     for k, lib in libs.items():
