@@ -862,13 +862,17 @@ static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint
 constexpr uint32_t kSpanMinAlloc = 10u * 1024u;
 static_assert(kSpanMinAlloc >= kVrLdsBytes, "an overflowing tile is streamed through its window");
 
+constexpr uint32_t kLdsPerCu = 160u * 1024u;
+
 static uint32_t span_window(uint64_t n, uint64_t key_bytes) {
   if (key_bytes == 0 || n == 0) return kSpanAlloc;
   const double span = 64.0 * (double)key_bytes / (double)n;
   const double w = span * 1.1 + 512.0 + kSpanPad;
   if (w >= (double)kSpanAlloc) return kSpanAlloc;
-  const uint32_t lds = ((uint32_t)w + 255u) & ~255u;
-  return lds < kSpanMinAlloc ? kSpanMinAlloc : lds;
+  uint32_t lds = (uint32_t)w < kSpanMinAlloc ? kSpanMinAlloc : (uint32_t)w;
+  // then the largest window that keeps as many tiles per CU (fewer overflows)
+  lds = (kLdsPerCu / (kLdsPerCu / lds)) & ~1023u;
+  return lds < kSpanMinAlloc ? kSpanMinAlloc : (lds > kSpanAlloc ? kSpanAlloc : lds);
 }
 
 // Fixed lengths: a tile's span is at most 64 * key_len + 15 bytes, so the LDS
