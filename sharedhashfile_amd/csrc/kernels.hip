@@ -30,6 +30,7 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "murmur3_mix.h"
@@ -776,7 +777,10 @@ __global__ __launch_bounds__(64) void k_vround(const uint8_t* __restrict__ bytes
   vround_tile<OUT>(bytes, key, valid, start, len, seed, sink, lds);
 }
 
-template <int OUT, bool VAR, int PIECES>
+// RFB: a variable-length tile whose span overflows the window is streamed in
+// rounds through the window (vround_tile, needs kVrLdsBytes of it); without,
+// hashed per lane from HBM (small windows, whose kernel then needs fewer VGPRs).
+template <int OUT, bool VAR, int PIECES, bool RFB = true>
 __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets,
                                              uint64_t off_base, uint32_t key_len, uint64_t n, uint32_t seed,
                                              uint32_t cap, Sink sink) {
@@ -793,7 +797,7 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
       const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
       store_result<OUT>(sink, ti.key, hash_lds(span_lds, p, ti.len, seed));
     }
-  } else if constexpr (VAR) {  // span over the window: stream it in rounds (vround_tile) instead
+  } else if constexpr (VAR && RFB) {  // span over the window: stream it in rounds (vround_tile) instead
     vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, reinterpret_cast<uint8_t*>(span_lds));
   } else if (ti.valid) {
     store_result<OUT>(sink, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
@@ -841,12 +845,12 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap) {
   return (unsigned)g;
 }
 
-template <int OUT, bool VAR, int PIECES>
+template <int OUT, bool VAR, int PIECES, bool RFB = true>
 static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
                                 uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint32_t lds) {
   const uint64_t tiles = (n + 63) / 64;
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;  // 137 G keys per launch
-  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES>), dim3((unsigned)tiles), dim3(64), lds, st,
+  hipLaunchKernelGGL((k_span<OUT, VAR, PIECES, RFB>), dim3((unsigned)tiles), dim3(64), lds, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, key_len, n, seed, lds - kSpanPad,
                      sink);
   return hipGetLastError();
@@ -854,25 +858,31 @@ static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint
 
 // LDS window per 64-key tile of a variable-length batch. Unknown byte count:
 // 20 KiB (8 tiles per CU; config D's U[8,512] spans average 16.6 KB). Known
-// (key_bytes = offsets[n] - offsets[0]): the tile's expected span, 64 x the
-// mean key length, plus a tenth and 512 B, between 10 KiB (what the round
-// fallback of an overflowing tile needs) and 20 KiB. Smaller windows keep more
-// tiles in flight per CU: at 10 vs 20 KiB U[8,128] keys run at 5.11 vs 3.38
-// TB/s, U[8,256] at 5.66 vs 4.27 (profiles/r1/ab_window/).
-constexpr uint32_t kSpanMinAlloc = 10u * 1024u;
-static_assert(kSpanMinAlloc >= kVrLdsBytes, "an overflowing tile is streamed through its window");
-
+// (key_bytes = offsets[n] - offsets[0]): at least the tile's expected span,
+// 64 x the mean key length, plus a tenth and 512 B; then grown to the most LDS
+// per tile that keeps as many tiles per CU (the LDS and register limits) and
+// that the instantiation's PIECES 1-KiB fetches cover. A CU holds 160 KiB /
+// window tiles, and a tile's window only loads while its span is in flight:
+// smaller windows keep more spans in flight (U[8,128] keys: 5.17 vs 3.39 TB/s
+// at 10 vs 20 KiB, profiles/r1/ab_window/, ab_sized/).
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
-static uint32_t span_window(uint64_t n, uint64_t key_bytes) {
-  if (key_bytes == 0 || n == 0) return kSpanAlloc;
-  const double span = 64.0 * (double)key_bytes / (double)n;
-  const double w = span * 1.1 + 512.0 + kSpanPad;
-  if (w >= (double)kSpanAlloc) return kSpanAlloc;
-  uint32_t lds = (uint32_t)w < kSpanMinAlloc ? kSpanMinAlloc : (uint32_t)w;
-  // then the largest window that keeps as many tiles per CU (fewer overflows)
-  lds = (kLdsPerCu / (kLdsPerCu / lds)) & ~1023u;
-  return lds < kSpanMinAlloc ? kSpanMinAlloc : (lds > kSpanAlloc ? kSpanAlloc : lds);
+template <int OUT, int PIECES, bool RFB>
+static hipError_t launch_var_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
+                                  uint32_t seed, const Sink& sink, hipStream_t st, uint32_t need) {
+  static const uint32_t reg_tiles = [] {  // tiles per CU the kernel's registers allow
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_span<OUT, true, PIECES, RFB>),
+                                                     64, 0) != hipSuccess || b < 1)
+      b = 1;
+    return (uint32_t)b;
+  }();
+  const uint32_t top = std::min<uint32_t>((uint32_t)PIECES * 1024u + kSpanPad, kSpanAlloc);
+  uint32_t tiles = std::min<uint32_t>(kLdsPerCu / need, reg_tiles);
+  if (tiles < 1) tiles = 1;
+  uint32_t lds = (kLdsPerCu / tiles) & ~255u;
+  lds = std::min(std::max(lds, need), top);
+  return launch_span_p<OUT, true, PIECES, RFB>(bytes, offsets, off_base, 0, n, seed, sink, st, lds);
 }
 
 // Fixed lengths: a tile's span is at most 64 * key_len + 15 bytes, so the LDS
@@ -881,10 +891,15 @@ template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
                               uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0) {
   if constexpr (VAR) {
-    const uint32_t lds = span_window(n, key_bytes);
-    if (lds - kSpanPad <= 10u * 1024u)
-      return launch_span_p<OUT, VAR, 10>(bytes, offsets, off_base, 0, n, seed, sink, st, lds);
-    return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, lds);
+    const double need = key_bytes && n ? 64.0 * (double)key_bytes / (double)n * 1.1 + 512.0 + kSpanPad : 1e30;
+    if (need >= (double)kSpanAlloc)
+      return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, kSpanAlloc);
+    const uint32_t w = (uint32_t)need;
+    // (PIECES 6 and 8 spill to scratch under hipcc 7.2; 4 and 10 take 55 and 47 VGPRs: 8 waves per SIMD)
+    if (w <= 4096u + kSpanPad) return launch_var_span<OUT, 4, false>(bytes, offsets, off_base, n, seed, sink, st, w);
+    if (w <= 10240u + kSpanPad) return launch_var_span<OUT, 10, false>(bytes, offsets, off_base, n, seed, sink, st, w);
+    static_assert(10240u + kSpanPad >= kVrLdsBytes, "windows with the round fallback hold its LDS");
+    return launch_var_span<OUT, kSpanPiecesMax, true>(bytes, offsets, off_base, n, seed, sink, st, w);
   } else {
     const uint32_t span = ((uint32_t)key_len * 64u + 15u + 15u) & ~15u;
     const uint32_t lds = (span + kSpanPad + 255u) & ~255u;
