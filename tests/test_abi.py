@@ -95,6 +95,14 @@ def test_argument_validation_needs_no_device(hb):
                                                  hbmod.KERNEL_TILED, None) == hbmod.ERR_ARG
     assert lib.shf_hash_batch_fixed_kernel_async(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 9,
                                                  None) == hbmod.ERR_ARG
+    # sized variable-length entry points
+    assert lib.shf_hash_batch_var_sized_async(None, None, 0, 0, 12345, None, None) == hbmod.OK
+    assert lib.shf_hash_batch_var_sized_async(keys.ctypes.data, None, 2, 16, 12345, out.ctypes.data,
+                                              None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_var_sized_kernel_async(keys.ctypes.data, keys.ctypes.data, 2, 16, 12345, None,
+                                                     hbmod.KERNEL_SPAN, None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_var_sized_kernel_async(keys.ctypes.data, keys.ctypes.data, 2, 16, 12345,
+                                                     out.ctypes.data, hbmod.KERNEL_TILED, None) == hbmod.ERR_ARG
     # row pre-probe: no index / no output / bad handles
     assert lib.shf_probe_batch_fixed_async(None, keys.ctypes.data, 16, 4, 12345, None, out.ctypes.data,
                                            None) == hbmod.ERR_ARG
@@ -127,6 +135,10 @@ def test_no_device_fails_loudly_not_on_cpu(hb):
         hbmod.hash_fixed_host(keys.reshape(4, 16))
     assert lib.shf_hash_batch_fixed_multi(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, 0) in (
         hbmod.ERR_NODEV, hbmod.ERR_HIP)
+    off = np.array([0, 16, 32], dtype=np.uint64)
+    assert lib.shf_hash_batch_var_sized_async(keys.ctypes.data, off.ctypes.data, 2, 32, 12345, out.ctypes.data,
+                                              None) in (hbmod.ERR_NODEV, hbmod.ERR_HIP)
+    assert not out.any()
     h = ctypes.c_void_p()
     assert lib.shf_row_index_create(4, ctypes.byref(h)) in (hbmod.ERR_NODEV, hbmod.ERR_HIP)
     assert h.value is None
