@@ -78,16 +78,21 @@ __device__ __forceinline__ ProbeLoc probe_locate(const Sink& k, const State& s) 
   return p;
 }
 
-__device__ __forceinline__ u32x4 probe_scan(const Sink& k, const ProbeLoc& p) {
+__device__ __forceinline__ bool probe_indexed(const Sink& k, const ProbeLoc& p) {
+  return p.e != kProbeNone && (uint64_t)(p.e >> 11) < k.n_slots;
+}
+
+// The key's row, or the stand-in when its tab is not indexed.
+__device__ __forceinline__ uintptr_t probe_row_addr(const Sink& k, const ProbeLoc& p) {
+  return probe_indexed(k, p) ? reinterpret_cast<uintptr_t>(k.rows) + ((uint64_t)(p.e >> 11) << kRowsPerTabShift) +
+                                   (p.row << 7)
+                             : reinterpret_cast<uintptr_t>(k.tab_slot);
+}
+
+// The 16 compares of a row already in registers, and the record.
+__device__ __forceinline__ u32x4 probe_match(const Sink& k, const ProbeLoc& p, const u32x4 (&v)[8]) {
   const uint32_t slot = p.e >> 11;
-  const bool indexed = p.e != kProbeNone && (uint64_t)slot < k.n_slots;
-  const uintptr_t at = indexed ? reinterpret_cast<uintptr_t>(k.rows) + ((uint64_t)slot << kRowsPerTabShift) +
-                                     (p.row << 7)
-                               : reinterpret_cast<uintptr_t>(k.tab_slot);
-  const g_u32x4* r = reinterpret_cast<const g_u32x4*>(at);
-  u32x4 v[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = r[q];
+  const bool indexed = probe_indexed(k, p);
   uint32_t mask = 0, pos = 0, first = 0;
 #pragma unroll
   for (int q = 7; q >= 0; --q) {  // descending: the lowest matching ref is written last
@@ -110,6 +115,14 @@ __device__ __forceinline__ u32x4 probe_scan(const Sink& k, const ProbeLoc& p) {
     rec.w = slot;
   }
   return rec;
+}
+
+__device__ __forceinline__ u32x4 probe_scan(const Sink& k, const ProbeLoc& p) {
+  const g_u32x4* r = reinterpret_cast<const g_u32x4*>(probe_row_addr(k, p));
+  u32x4 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = r[q];
+  return probe_match(k, p, v);
 }
 
 __device__ __forceinline__ u32x4 probe_row(const Sink& k, const State& s) { return probe_scan(k, probe_locate(k, s)); }
@@ -164,6 +177,9 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 #endif
 constexpr uint32_t kF16Block = SHFHB_F16_BLOCK;
 constexpr uint32_t kF16Kpl = SHFHB_F16_KPL;
+#ifndef SHFHB_PROBE_LDS
+#define SHFHB_PROBE_LDS 1  // cooperative row fetch + LDS transpose: +2.7 % at 10M keys (profiles/r1/ab_probe_lds/)
+#endif
 #ifndef SHFHB_PROBE_KPL
 #define SHFHB_PROBE_KPL 1  // keys per lane of the fused hash + row pre-probe (2 and 4 measured ~2 % slower)
 #endif
@@ -195,8 +211,40 @@ __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__
       finish(s[j], 16);
       p[j] = probe_locate(sink, s[j]);
     }
+#if SHFHB_PROBE_LDS
+    // Rows fetched cooperatively, 8 lanes per row (each load instruction then
+    // touches 8 full 128-B lines instead of 64 partial ones), transposed
+    // through 8 KiB of LDS per wave (XOR-swizzled, conflict-free), then each
+    // lane scans its own row.
+    static_assert(kpl == 1, "one key per lane");
+    __shared__ u32x4 rows_lds[kF16Block * 8];
+    const uint32_t lane = threadIdx.x & 63u;
+    u32x4* L = rows_lds + (threadIdx.x & ~63u) * 8u;
+    const uint64_t at = probe_row_addr(sink, p[0]);
+    const int alo = (int)(uint32_t)at, ahi = (int)(uint32_t)(at >> 32);
+    u32x4 g[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+      const int src = (int)(8u * q + (lane >> 3));
+      const uint64_t a = (uint64_t)(uint32_t)__shfl(alo, src) | ((uint64_t)(uint32_t)__shfl(ahi, src) << 32);
+      g[q] = *reinterpret_cast<const g_u32x4*>(a + 16u * (lane & 7u));
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+      const uint32_t src = 8u * q + (lane >> 3);
+      L[src * 8u + ((lane & 7u) ^ (src & 7u))] = g[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    u32x4 v[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) v[q] = L[lane * 8u + (q ^ (lane & 7u))];
+    rec[0] = probe_match(sink, p[0], v);
+#else
 #pragma unroll
     for (uint32_t j = 0; j < kpl; ++j) rec[j] = probe_scan(sink, p[j]);
+#endif
 #pragma unroll
     for (uint32_t j = 0; j < kpl; ++j) {
       const uint64_t i = i0 + j * kF16Block;
