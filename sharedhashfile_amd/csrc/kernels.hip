@@ -127,6 +127,40 @@ __device__ __forceinline__ u32x4 probe_scan(const Sink& k, const ProbeLoc& p) {
 
 __device__ __forceinline__ u32x4 probe_row(const Sink& k, const State& s) { return probe_scan(k, probe_locate(k, s)); }
 
+#ifndef SHFHB_PROBE_LDS
+#define SHFHB_PROBE_LDS 1  // cooperative row fetch + LDS transpose: +3 % (profiles/r1/ab_probe_lds/)
+#endif
+
+// probe_scan for a whole wave (every lane must call it): the rows are fetched
+// 8 lanes per row, so each of the 8 load instructions touches 8 whole 128-B
+// lines instead of 64 partial ones (row addresses move by __shfl), then
+// transposed through `lds` (8 KiB for this wave, XOR-swizzled so both the
+// ds_write_b128 and the ds_read_b128 are conflict-free) for the lane's compares.
+__device__ __forceinline__ u32x4 probe_scan_coop(const Sink& k, const ProbeLoc& p, u32x4* lds) {
+  const uint32_t lane = __lane_id();
+  const uint64_t at = probe_row_addr(k, p);
+  const int alo = (int)(uint32_t)at, ahi = (int)(uint32_t)(at >> 32);
+  u32x4 g[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {
+    const int src = (int)(8u * q + (lane >> 3));
+    const uint64_t a = (uint64_t)(uint32_t)__shfl(alo, src) | ((uint64_t)(uint32_t)__shfl(ahi, src) << 32);
+    g[q] = *reinterpret_cast<const g_u32x4*>(a + 16u * (lane & 7u));
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t src = 8u * q + (lane >> 3);
+    lds[src * 8u + ((lane & 7u) ^ (src & 7u))] = g[q];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  u32x4 v[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) v[q] = lds[lane * 8u + (q ^ (lane & 7u))];
+  return probe_match(k, p, v);
+}
+
 __device__ __forceinline__ void store_probe(const Sink& sink, uint64_t i, const State& s, const u32x4& rec) {
   if (sink.hash_out) {
     const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
@@ -152,10 +186,19 @@ __device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const
 // ballots and ds_bpermute -- measured 3.9x slower: profiles/r1/ab_probe_coop_vs_lane_*.txt.)
 __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ hashes, uint64_t n, Sink sink) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#if SHFHB_PROBE_LDS
+  __shared__ u32x4 rows_lds[256 * 8];
+  u32x4 h = {0u, 0u, 0u, 0u};  // lanes past n still take part in the wave's row fetch
+  if (i < n) h = __builtin_nontemporal_load(&hashes[i]);
+  const State s{pack64(h.x, h.y), pack64(h.z, h.w)};
+  const u32x4 rec = probe_scan_coop(sink, probe_locate(sink, s), rows_lds + (threadIdx.x & ~63u) * 8u);
+  if (i < n) reinterpret_cast<u32x4*>(sink.out)[i] = rec;
+#else
   if (i >= n) return;
   const u32x4 h = __builtin_nontemporal_load(&hashes[i]);
   const State s{pack64(h.x, h.y), pack64(h.z, h.w)};
   reinterpret_cast<u32x4*>(sink.out)[i] = probe_row(sink, s);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -177,9 +220,6 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 #endif
 constexpr uint32_t kF16Block = SHFHB_F16_BLOCK;
 constexpr uint32_t kF16Kpl = SHFHB_F16_KPL;
-#ifndef SHFHB_PROBE_LDS
-#define SHFHB_PROBE_LDS 1  // cooperative row fetch + LDS transpose: +2.7 % at 10M keys (profiles/r1/ab_probe_lds/)
-#endif
 #ifndef SHFHB_PROBE_KPL
 #define SHFHB_PROBE_KPL 1  // keys per lane of the fused hash + row pre-probe (2 and 4 measured ~2 % slower)
 #endif
@@ -212,35 +252,9 @@ __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__
       p[j] = probe_locate(sink, s[j]);
     }
 #if SHFHB_PROBE_LDS
-    // Rows fetched cooperatively, 8 lanes per row (each load instruction then
-    // touches 8 full 128-B lines instead of 64 partial ones), transposed
-    // through 8 KiB of LDS per wave (XOR-swizzled, conflict-free), then each
-    // lane scans its own row.
     static_assert(kpl == 1, "one key per lane");
     __shared__ u32x4 rows_lds[kF16Block * 8];
-    const uint32_t lane = threadIdx.x & 63u;
-    u32x4* L = rows_lds + (threadIdx.x & ~63u) * 8u;
-    const uint64_t at = probe_row_addr(sink, p[0]);
-    const int alo = (int)(uint32_t)at, ahi = (int)(uint32_t)(at >> 32);
-    u32x4 g[8];
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) {
-      const int src = (int)(8u * q + (lane >> 3));
-      const uint64_t a = (uint64_t)(uint32_t)__shfl(alo, src) | ((uint64_t)(uint32_t)__shfl(ahi, src) << 32);
-      g[q] = *reinterpret_cast<const g_u32x4*>(a + 16u * (lane & 7u));
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) {
-      const uint32_t src = 8u * q + (lane >> 3);
-      L[src * 8u + ((lane & 7u) ^ (src & 7u))] = g[q];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    u32x4 v[8];
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) v[q] = L[lane * 8u + (q ^ (lane & 7u))];
-    rec[0] = probe_match(sink, p[0], v);
+    rec[0] = probe_scan_coop(sink, p[0], rows_lds + (threadIdx.x & ~63u) * 8u);
 #else
 #pragma unroll
     for (uint32_t j = 0; j < kpl; ++j) rec[j] = probe_scan(sink, p[j]);
