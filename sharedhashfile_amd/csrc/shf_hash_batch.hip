@@ -225,11 +225,18 @@ bool is_host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// memcpy split over a few threads: one core cannot keep up with PCIe.
+// memcpy split over a few threads (SHF_HB_COPY_THREADS, default 8, read per
+// call): one core cannot keep up with PCIe.
+size_t copy_threads() {
+  const char* e = getenv("SHF_HB_COPY_THREADS");
+  const long v = e ? strtol(e, nullptr, 10) : 0;
+  return v >= 1 && v <= 64 ? (size_t)v : 8;
+}
+
 void par_memcpy(void* dst, const void* src, size_t n) {
-  constexpr size_t kMinPerThread = (size_t)4 << 20;
+  constexpr size_t kMinPerThread = (size_t)2 << 20;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t t = std::min<size_t>({(size_t)8, (size_t)hw, std::max<size_t>(1, n / kMinPerThread)});
+  const size_t t = std::min<size_t>({copy_threads(), (size_t)hw, std::max<size_t>(1, n / kMinPerThread)});
   if (t <= 1) {
     memcpy(dst, src, n);
     return;

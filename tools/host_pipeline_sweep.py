@@ -48,10 +48,14 @@ def main():
     digests = {}
     print("G keys/s, host buffers in and out (%d x 16 B keys; %d x U[8,512] B keys, %.0f MB)" % (n, m, off[-1] / 1e6))
     print("%8s %5s %18s %18s %18s" % ("stage_MB", "slots", "16B pageable", "16B pinned", "var pageable"))
-    for mb in (4, 8, 16, 32, 64):
-        for slots in (2, 3, 4):
+    shapes = [(mb, slots, 8) for mb in (4, 8, 16, 32, 64) for slots in (2, 3, 4)]
+    if len(sys.argv) > 1 and sys.argv[1] == "--threads":  # staging-copy threads at the default shape
+        shapes = [(32, 3, t) for t in (2, 4, 8, 12, 16, 24)]
+        print("(rows: SHF_HB_COPY_THREADS = 2, 4, 8, 12, 16, 24 at 32 MiB x 3 slots)")
+    for mb, slots, threads in shapes:
             os.environ["SHF_HB_STAGE_MB"] = str(mb)
             os.environ["SHF_HB_SLOTS"] = str(slots)
+            os.environ["SHF_HB_COPY_THREADS"] = str(threads)
             row = []
             for kind, mem, count, fn, res in cases:
                 rc = fn()  # warm: staging buffers for this shape
@@ -67,7 +71,7 @@ def main():
                 d = hashlib.sha256(np.ascontiguousarray(res()).tobytes()).hexdigest()
                 assert digests.setdefault(kind, d) == d, (kind, mem, mb, slots)
                 row.append("%18.3f" % (count / dt / 1e9))
-            print("%8d %5d %s" % (mb, slots, " ".join(row)), flush=True)
+            print("%8d %5d %s  threads=%d" % (mb, slots, " ".join(row), threads), flush=True)
     print("hashes identical across shapes:", {k: v[:16] for k, v in digests.items()})
 
 
