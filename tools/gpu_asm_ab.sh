@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical: SHFHB_ASM_MIX=1 is now the default, so `asm` equals `base`
+# (profiles/r1/ab_asm/ has the A/B from when it was not).
 # Mix arithmetic variant (SHFHB_ASM_MIX=1: alignbit rotates, shift-add *5) against
 # the compiler's lowering, on every hashing kernel that the bench lines use.
 #   python tools/ab.py --prebuild build/ab --variant asm=-DSHFHB_ASM_MIX=1

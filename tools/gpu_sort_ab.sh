@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical: the sorted span kernel lost and was removed (profiles/r1/ab_sort/);
+# rerunning needs its source from git history (commit 1d01bbc).
 # Sorted span kernel (SHFHB_SPAN_SORT_W = 2 or 4 waves per workgroup, keys hashed
 # in block-count order; sort2asm adds SHFHB_ASM_MIX=1) against k_span: kernel 4
 # in every variant, ~6.5 GB of variable-length keys U[lo, hi] per distribution.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical: SHFHB_SPAN_ALLOC was a one-off build flag (profiles/r1/ab_window/);
+# the window is now sized per launch (kernels.hip launch_span).
 # k_span LDS window per tile (SHFHB_SPAN_ALLOC bytes: 16384 -> 10 tiles per CU,
 # 18176 -> 9, 20480 -> 8 (base), 23296 -> 7, 27264 -> 6) per length distribution.
 #   python tools/ab.py --prebuild build/ab --variant w16=-DSHFHB_SPAN_ALLOC=16384 ...

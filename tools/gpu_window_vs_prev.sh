@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical: build/ab/lib_prev.so was built from commit 97e06d7's csrc
+# (profiles/r1/ab_sized_small/vs_prev_*).
 # Sized windows: the current rule (small windows without the round fallback,
 # 4/10-KiB fetches) against the previous one (10-20 KiB, round fallback), same
 # process, kernel AUTO with the byte count. build/ab/lib_prev.so = commit 97e06d7.
