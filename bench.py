@@ -5,19 +5,32 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 A "step" is one launch of the hashing kernel over one whole batch of synthetic
-keys already resident in HBM (the batch is regenerated on device before timing,
-never inside the timed region).
+keys already resident in HBM (batches are generated on device before the timed
+region, never inside it).
 
 Headline (`value`): BASELINE.json configs[1] = 10M fixed 16-byte keys per GPU,
 MurmurHash3_x64_128 seed 12345 (= shf_make_hash, /root/reference/src/shf.c:456)
--> 16-byte SHF_HASH per key. Also reported (`secondary`): configs[2] (100M x
-256-byte keys) and configs[3] (100M variable-length keys, 8..512 B), and the
-row pre-probe: the configs[1] keys hashed and probed against
-a device row index holding all of them (`probe16`).
+-> 16-byte SHF_HASH per key. The timed steps rotate over --rotate distinct
+batches (keys + outputs, 4 x 320 MB by default), so no step re-reads lines the
+previous step left in the 256 MiB Infinity Cache; the single-batch figure is
+the secondary `fixed16_hot`. Also reported (`secondary`): configs[4]'s 1B keys
+split over the job's GPUs (`shard1b`, strong scaling), configs[2] (100M x
+256-byte keys), configs[3] (100M variable-length keys, 8..512 B), and the row
+pre-probe (`probe16`).
 
-Multi-GPU: one process per GPU, each hashes its own independent shard (weak
-scaling); torch.distributed (RCCL) is used only for the start/stop barriers and
-the max-over-ranks of the elapsed time -- there is no collective on the data path.
+Every line: min / median / max over --repeats timed repeats of K steps each
+(`value` is the median), and after the timed region >= 20 000 sampled outputs
+of the timed batches are checked against the CPU oracle (the checker only;
+`verified`).
+
+Multi-GPU: one process per GPU, each hashes its own
+independent shard (no collective on the data path; torch.distributed is used
+only for the start/stop barriers and the max over ranks of the elapsed time).
+`--gpus N` without a torch.distributed launcher spawns the N rank processes
+itself before anything touches the GPU. Each rank needs a GPU of its own; a
+run with more ranks than visible GPUs is refused unless --allow-shared-gpu is
+given, and then the line says `"rehearsal": true` and `n_gpus` counts the
+distinct GPUs actually used.
 """
 import argparse
 import csv
@@ -25,6 +38,7 @@ import glob
 import json
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -37,48 +51,51 @@ sys.path.insert(0, ROOT)
 
 METRIC = "keys hashed/s device-resident (16 B & 256 B keys) + GiB/s vs HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E peak (spec)
+HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: best measured float4 copy
+SIMDS = 256 * 4        # 256 CUs x 4 SIMDs
+XCDS = 8
 SEED = 12345
 WARMUP_MIN_S = 0.25  # untimed warmup floor per workload (seconds of GPU work)
+VERIFY_SAMPLES = 20_000
+BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for worker pools)
 
-# algorithmic bytes per key = key bytes read + 16-byte SHF_HASH
-# written (+ 8-byte offset read for variable-length keys).
-KERNEL_NAMES = {"fixed16": "k_fixed16", "tiled": "k_tiled", "generic": "k_generic"}
+# rocprofv3 kernel-name substrings of each workload's kernel (PMC passes)
+KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
+               "fixed256": "k_tiled<0, 8>", "var": "k_span<0, true", "probe16": "k_fixed16<2>"}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None, help="GPUs (= ranks); default WORLD_SIZE or 1")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--repeats", type=int, default=3, help="timed repeats of --steps steps per line")
+    p.add_argument("--rotate", type=int, default=4, help="distinct 10M-key batches the headline rotates over")
     p.add_argument("--keys16", type=int, default=10_000_000, help="configs[1]: 16-B keys per GPU")
     p.add_argument("--keys1b", type=int, default=1_000_000_000,
                    help="configs[4]: 16-B keys for the whole job, split over the GPUs (strong scaling)")
     p.add_argument("--keys256", type=int, default=100_000_000, help="configs[2]: 256-B keys per GPU")
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
-    p.add_argument("--only", default="", help="comma list of fixed16,fixed256,var,probe16 (default: all)")
+    p.add_argument("--only", default="", help="comma list of fixed16,fixed16_hot,shard1b,fixed256,var,probe16")
     p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
     p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-threads", type=int, default=16, help="threads for cpu_baseline.all_cores (0/1: skip)")
+    p.add_argument("--no-verify", action="store_true", help="skip the sampled oracle check of the timed outputs")
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
-                   help="auto: at N=1 run two short rocprofv3 --pmc child passes for HBM bytes")
-    p.add_argument("--host-inclusive", action="store_true",
-                   help="also time the pinned host->device->host path (reported, never `value`)")
-    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                   help="backend for the barrier/max-reduce only (gloo: multi-rank rehearsal on one GPU)")
+                   help="auto: at N=1 run rocprofv3 --pmc child passes (HBM bytes, VALU busy) per kernel")
+    p.add_argument("--no-host-inclusive", action="store_true",
+                   help="skip the host-buffer (pinned/pageable hipMemcpyAsync both ways) leg at N=1")
+    p.add_argument("--host-keys", type=int, default=10_000_000, help="keys per host-inclusive batch")
+    p.add_argument("--allow-shared-gpu", action="store_true",
+                   help="rehearsal only: let ranks share GPUs (gloo barriers; the line is marked rehearsal)")
+    p.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="backend for the barriers / max-reduce only (auto: nccl, gloo when GPUs are shared)")
     p.add_argument("--warmup-min-s", type=float, default=WARMUP_MIN_S,
                    help="keep warming up (untimed) until this many seconds of the workload have run")
     p.add_argument("--quiet", action="store_true")
-    return p.parse_args()
-
-
-def dist_env():
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return rank, world, local
+    return p.parse_args(argv)
 
 
 def log(args, *a):
@@ -87,14 +104,78 @@ def log(args, *a):
 
 
 # ---------------------------------------------------------------------------
+# launch: one process per GPU
+# ---------------------------------------------------------------------------
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    return rank, world, local, local_world
+
+
+def plan_device(local_rank, local_world, device_count, allow_shared):
+    """(device index, shared) for this rank: one distinct GPU per local rank, or
+    a refusal. Sharing (rank i on GPU i % count) only with allow_shared."""
+    if device_count < 1:
+        raise SystemExit("bench.py needs a GPU (HIP); none visible")
+    if local_world > device_count:
+        if not allow_shared:
+            raise SystemExit("bench.py: %d ranks on this node but only %d GPU(s) visible; every rank needs a GPU "
+                             "of its own (pass --allow-shared-gpu for a rehearsal, marked as such)"
+                             % (local_world, device_count))
+        return local_rank % device_count, True
+    return local_rank, False
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(argv, n):
+    """Start n rank processes of this script (RANK/WORLD_SIZE/... in their
+    environment) and wait for them. This process never touches the GPU: the
+    ranks are children, not an exec of a GPU-initialised process. The first
+    rank to fail stops the others (by PID)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------------------
 # workloads
 # ---------------------------------------------------------------------------
 class Workload:
-    """One device-resident batch and the launch that hashes it."""
+    """Device-resident batches and the launch that hashes one of them.
+    launch(i) hashes batch i % len(batches) into its own output."""
 
-    def __init__(self, name, n, bytes_per_key, launch, kernel, desc):
+    def __init__(self, name, n, bytes_per_key, launches, kernel, desc, verify=None):
         self.name, self.n, self.bytes_per_key = name, n, bytes_per_key
-        self.launch, self.kernel, self.desc = launch, kernel, desc
+        self.launches, self.kernel, self.desc, self.verify = launches, kernel, desc, verify
+        self.job_keys = None
+
+    def launch(self, i):
+        self.launches[i % len(self.launches)]()
 
 
 def fast_launch(hb, keys, key_len, n, out, kernel, dev):
@@ -117,22 +198,83 @@ def fast_launch(hb, keys, key_len, n, out, kernel, dev):
     return launch
 
 
+def _sample_idx(n, k, seed):
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, n, size=min(k, n), dtype=np.int64)
+    return np.unique(np.concatenate([idx, [0, n - 1]]))
+
+
+def verify_fixed(pairs, key_len, samples, seed):
+    """pairs: [(keys, out)] device tensors. Sampled keys of every pair, hashed
+    by the CPU oracle (the checker), against the timed outputs."""
+    import torch
+
+    from oracle.oracle_py import Oracle
+
+    o = Oracle()
+    per = max(1, samples // len(pairs))
+    checked = 0
+    for j, (keys, out) in enumerate(pairs):
+        n = out.shape[0]
+        idx = _sample_idx(n, per, seed + j)
+        ti = torch.from_numpy(idx).to(keys.device)
+        k = keys.view(n, key_len).index_select(0, ti).cpu().numpy()
+        got = out.index_select(0, ti).cpu().numpy().view(np.uint64)
+        if not np.array_equal(got, o.hash_fixed(k, key_len)):
+            return False, checked
+        checked += idx.size
+    return True, checked
+
+
+def verify_var(data, off, out, samples, seed):
+    import torch
+
+    from oracle.oracle_py import Oracle
+
+    n = out.shape[0]
+    idx = _sample_idx(n, samples, seed)
+    ti = torch.from_numpy(idx).to(data.device)
+    o0, o1 = off.index_select(0, ti), off.index_select(0, ti + 1)
+    lens = o1 - o0
+    starts = torch.repeat_interleave(o0, lens)
+    first = torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+    pos = starts + (torch.arange(starts.numel(), device=data.device) - first)
+    sub = data.index_select(0, pos).cpu().numpy()
+    hoff = np.zeros(idx.size + 1, dtype=np.uint64)
+    hoff[1:] = np.cumsum(lens.cpu().numpy())
+    got = out.index_select(0, ti).cpu().numpy().view(np.uint64)
+    return bool(np.array_equal(got, Oracle().hash_var(sub, hoff))), int(idx.size)
+
+
 def make_workloads(args, dev, rank, world=1):
     import torch
 
     import sharedhashfile_amd as hb
     from sharedhashfile_amd.keygen import device_random_bytes
 
-    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed256", "var", "probe16", "shard1b"}
+    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed16_hot", "shard1b", "fixed256", "var",
+                                                        "probe16"}
     wl = []
     seed_base = 0x5348460000000001 + 1000 * rank
-    if "fixed16" in only:
+    fk16 = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
+    if "fixed16" in only or "fixed16_hot" in only:
         n = args.keys16
-        keys = device_random_bytes(n * 16, seed_base + 1, dev)
-        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
-        fk = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
-        wl.append(Workload("fixed16", n, 16 + 16, fast_launch(hb, keys, 16, n, out, fk, dev),
-                           "k_fixed16", "%d fixed 16-B keys" % n))
+        B = max(1, args.rotate)
+        pairs = []
+        for b in range(B):
+            keys = device_random_bytes(n * 16, seed_base + 1 + 100 * b, dev)
+            pairs.append((keys, torch.empty((n, 2), dtype=torch.int64, device=dev)))
+        if "fixed16" in only:
+            wl.append(Workload("fixed16", n, 16 + 16, [fast_launch(hb, k, 16, n, o, fk16, dev) for k, o in pairs],
+                               "k_fixed16", "%d fixed 16-B keys per step, rotating over %d distinct batches "
+                               "(%.2f GB of keys + hashes)" % (n, B, B * n * 32 / 1e9),
+                               lambda p=pairs: verify_fixed(p, 16, VERIFY_SAMPLES, 11)))
+        if "fixed16_hot" in only:
+            k0, o0 = pairs[0]
+            wl.append(Workload("fixed16_hot", n, 16 + 16, [fast_launch(hb, k0, 16, n, o0, fk16, dev)], "k_fixed16",
+                               "%d fixed 16-B keys, the same batch every step (its 320 MB partly stay in the "
+                               "256 MiB Infinity Cache)" % n,
+                               lambda p=pairs[:1]: verify_fixed(p, 16, VERIFY_SAMPLES, 12)))
     if "shard1b" in only:
         # configs[4]: 1B 16-B keys split evenly over the job's GPUs (strong scaling:
         # 1B / world keys on this rank, contiguous index range, no collective).
@@ -143,18 +285,20 @@ def make_workloads(args, dev, rank, world=1):
         n = hi - lo
         keys = device_random_bytes(n * 16, seed_base + 6, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
-        w = Workload("shard1b", n, 16 + 16, fast_launch(hb, keys, 16, n, out, 0, dev),
-                     "k_fixed16", "%d 16-B keys split over %d GPU(s): keys [%d, %d) on rank %d" % (total, world, lo, hi, rank))
+        w = Workload("shard1b", n, 16 + 16, [fast_launch(hb, keys, 16, n, out, 0, dev)], "k_fixed16",
+                     "%d 16-B keys split over %d rank(s): keys [%d, %d) on rank %d" % (total, world, lo, hi, rank),
+                     lambda p=[(keys, out)]: verify_fixed(p, 16, VERIFY_SAMPLES, 13))
         w.job_keys = total
+        w.shard = (lo, hi)
         wl.append(w)
     if "fixed256" in only:
         n = args.keys256
         keys = device_random_bytes(n * 256, seed_base + 2, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         fk = {"auto": 0, "fixed16": 2, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
-        wl.append(Workload("fixed256", n, 256 + 16,
-                           lambda k=keys, o=out, fk=fk: hb.hash_fixed(k, 256, out=o, kernel=fk),
-                           "k_tiled", "%d fixed 256-B keys" % n))
+        wl.append(Workload("fixed256", n, 256 + 16, [fast_launch(hb, keys, 256, n, out, fk, dev)],
+                           "k_tiled", "%d fixed 256-B keys" % n,
+                           lambda p=[(keys, out)]: verify_fixed(p, 256, VERIFY_SAMPLES, 14)))
     if "var" in only:
         n = args.keysvar
         g = torch.Generator(device=dev)
@@ -166,10 +310,13 @@ def make_workloads(args, dev, rank, world=1):
         data = device_random_bytes(total, seed_base + 4, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         del lens
+        vk = {"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]
         wl.append(Workload("var", n, total / n + 8 + 16,
-                           lambda d=data, o=off, out=out, vk={"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]:
-                           hb.hash_var(d, o, out=out, kernel=vk, key_bytes=total),
-                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel, "k_span"), "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9)))
+                           [lambda d=data, o=off, out=out: hb.hash_var(d, o, out=out, kernel=vk, key_bytes=total)],
+                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel,
+                                                                                               "k_span"),
+                           "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9),
+                           lambda: verify_var(data, off, out, VERIFY_SAMPLES, 15)))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding
         # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +
@@ -181,91 +328,181 @@ def make_workloads(args, dev, rank, world=1):
         h = hb.hash_fixed(keys, 16)
         tab_slot, rows, n_slots, placed = synthetic_index(h, tabs_per_win=args.probe_tabs)
         index = hb.RowIndex(n_slots, tab_slot, rows)
+        host_index = (tab_slot.cpu().numpy().view(np.uint32), rows.cpu().numpy(), n_slots)
         del h, tab_slot, rows
         out = torch.empty((n, 4), dtype=torch.int32, device=dev)
-        wl.append(Workload("probe16", n, 16 + 128 + 16 + 4 * 256 * 2048 / n,
-                           lambda k=keys, o=out, ix=index: hb.probe_fixed(ix, k, 16, out=o),
-                           "k_fixed16<kOutProbe>", "%d fixed 16-B keys hashed and probed against a row index of "
-                           "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed)))
-        wl[-1].index = index
+
+        def verify_probe(keys=keys, out=out, hx=host_index):
+            import torch as _t
+
+            from oracle.oracle_py import Oracle
+
+            o = Oracle()
+            idx = _sample_idx(n, VERIFY_SAMPLES, 16)
+            ti = _t.from_numpy(idx).to(dev)
+            k = keys.view(n, 16).index_select(0, ti).cpu().numpy()
+            want = o.probe(o.hash_fixed(k, 16), hx[0], hx[1], hx[2])
+            got = out.index_select(0, ti).cpu().numpy().view(np.uint32)
+            return bool(np.array_equal(got, want)), int(idx.size)
+
+        w = Workload("probe16", n, 16 + 128 + 16 + 4 * 256 * 2048 / n,
+                     [lambda k=keys, o=out, ix=index: hb.probe_fixed(ix, k, 16, out=o)],
+                     "k_fixed16<kOutProbe>", "%d fixed 16-B keys hashed and probed against a row index of "
+                     "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed), verify_probe)
+        w.index = index
+        wl.append(w)
     torch.cuda.synchronize()
     return wl
 
 
-def time_workload(w, steps, warmup, dist, warmup_min_s=WARMUP_MIN_S):
-    """Returns (wall seconds for `steps` steps, max over ranks; mean per-launch
-    kernel seconds from HIP events on the launch stream)."""
+def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP_MIN_S):
+    """Per repeat: (wall seconds for `steps` steps, max over ranks; mean per-launch
+    device seconds from HIP events on the launch stream, max over ranks)."""
     import torch
 
     stream = torch.cuda.current_stream()  # the stream every launch goes to (hb passes it to the library)
     # W warmup steps, continued (untimed) until the GPU has run this workload
-    # for WARMUP_MIN_S: after seconds of host-side setup the clocks start low,
+    # for warmup_min_s: after seconds of host-side setup the clocks start low,
     # and 10 steps of a 50-us kernel are not enough to bring them up.
     t_w = time.perf_counter()
     done = 0
     while done < warmup or time.perf_counter() - t_w < warmup_min_s:
-        w.launch()
+        w.launch(done)
         done += 1
         if done >= warmup and done % 16 == 0:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    walls, devs, enq = [], [], []
+    for _ in range(repeats):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(steps):
+            w.launch(i)
+        ev1.record(stream)
+        t_enq = time.perf_counter()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        walls.append(t1 - t0)
+        # HIP events bracketing the timed region on the launch stream: mean device
+        # time per launch, back-to-back kernels (inter-kernel gaps included)
+        devs.append(ev0.elapsed_time(ev1) / steps / 1e3)
+        enq.append(t_enq - t0)
     if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        w.launch()
-    ev1.record(stream)
-    t_enq = time.perf_counter()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    w.enqueue_s = t_enq - t0  # host time to enqueue the steps (diagnostic)
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    # HIP events bracketing the timed region on the launch stream: mean device
-    # time per launch, back-to-back kernels (inter-kernel gaps included)
-    per_launch = ev0.elapsed_time(ev1) / steps / 1e3
-    if dist:
-        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([elapsed, per_launch], dtype=torch.float64, device=dev)
+        import torch as _t
+
+        t = _t.tensor(walls + devs, dtype=_t.float64, device=dist_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, per_launch = float(t[0]), float(t[1])
-    return elapsed, per_launch
+        walls, devs = [float(x) for x in t[:repeats]], [float(x) for x in t[repeats:]]
+    w.enqueue_s = float(np.median(enq))
+    return walls, devs
 
 
-def time_host_inclusive(args, n=10_000_000):
-    """Host buffers in and out (SHF_HASH_MEM_HOST): H2D keys + kernel + D2H
-    hashes, pipelined in SHF_HB_STAGE_MB chunks, SHF_HB_SLOTS in flight on their
-    own streams. Pageable buffers are staged through pinned memory; page-locked
-    ones are DMA'd directly."""
+# ---------------------------------------------------------------------------
+# host-inclusive rate: keys start and hashes end in host memory
+# ---------------------------------------------------------------------------
+def time_host_inclusive(args, dev):
+    """Host buffers in and out (SHF_HASH_MEM_HOST): H2D keys (+ offsets) +
+    kernel + D2H hashes, pipelined in SHF_HB_STAGE_MB chunks, SHF_HB_SLOTS in
+    flight. Pageable buffers are staged through pinned memory; page-locked
+    ones are DMA'd directly. Fixed 16-B keys and config-D's U[8,512] B
+    variable-length keys, --host-keys of each."""
     import torch
 
     import sharedhashfile_amd as hb
-    from sharedhashfile_amd.keygen import splitmix_bytes
+    from sharedhashfile_amd.keygen import device_random_bytes
 
     lib = hb.load()
-    keys = np.frombuffer(splitmix_bytes(n * 16, 77), dtype=np.uint8).copy()
-    res = {"keys": n, "key_len": 16, "unit": "keys/s"}
+    n = args.host_keys
+    res = {"unit": "keys/s", "note": "never `value`: PCIe-bound; sample = %d keys per batch, median of the "
+                                     "timed repeats after one untimed call" % n}
+    keys = device_random_bytes(n * 16, 77, dev).cpu().numpy()
+    g = torch.Generator(device=dev)
+    g.manual_seed(78)
+    lens = torch.randint(8, 513, (n,), generator=g, device=dev, dtype=torch.int64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens.cpu().numpy())
+    data = device_random_bytes(int(off[-1]), 79, dev).cpu().numpy()
+    del lens
     pk = torch.from_numpy(keys).pin_memory()
     po = torch.empty((n, 2), dtype=torch.int64).pin_memory()
     out = np.empty((n, 2), dtype=np.uint64)
-    for name, kp, op in [("pageable", keys.ctypes.data, out.ctypes.data), ("pinned", pk.data_ptr(), po.data_ptr())]:
-        assert lib.shf_hash_batch_fixed(kp, 16, n, SEED, op, hb.MEM_HOST) == 0
-        reps = 5
-        t0 = time.perf_counter()
+    pd = torch.from_numpy(data).pin_memory()
+    poff = torch.from_numpy(off.view(np.int64)).pin_memory()
+    vout = np.empty((n, 2), dtype=np.uint64)
+    vpo = torch.empty((n, 2), dtype=torch.int64).pin_memory()
+    cases = [
+        ("fixed16_pageable", lambda: lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, SEED, out.ctypes.data,
+                                                              hb.MEM_HOST), 5),
+        ("fixed16_pinned", lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED, po.data_ptr(), hb.MEM_HOST),
+         5),
+        ("var_pageable", lambda: lib.shf_hash_batch_var(data.ctypes.data, off.ctypes.data, n, SEED, vout.ctypes.data,
+                                                        hb.MEM_HOST), 3),
+        ("var_pinned", lambda: lib.shf_hash_batch_var(pd.data_ptr(), poff.data_ptr(), n, SEED, vpo.data_ptr(),
+                                                      hb.MEM_HOST), 3),
+    ]
+    for name, fn, reps in cases:
+        rc = fn()
+        if rc:
+            raise hb.ShfHashBatchError(rc, "host-inclusive " + name)
+        ts = []
         for _ in range(reps):
-            assert lib.shf_hash_batch_fixed(kp, 16, n, SEED, op, hb.MEM_HOST) == 0
-        dt = (time.perf_counter() - t0) / reps
-        res[name] = n / dt
+            t0 = time.perf_counter()
+            rc = fn()
+            ts.append(time.perf_counter() - t0)
+            if rc:
+                raise hb.ShfHashBatchError(rc, "host-inclusive " + name)
+        res[name] = {"value": n / float(np.median(ts)), "value_min": n / max(ts), "value_max": n / min(ts),
+                     "repeats": reps}
+    # sampled check of the host outputs (the oracle is the checker)
+    try:
+        from oracle.oracle_py import Oracle
+
+        o = Oracle()
+        idx = _sample_idx(n, VERIFY_SAMPLES, 21)
+        want = o.hash_fixed(keys.reshape(n, 16)[idx], 16)
+        ok = np.array_equal(out[idx], want) and np.array_equal(po.numpy().view(np.uint64)[idx], want)
+        sub_lens = (off[idx + 1] - off[idx]).astype(np.int64)
+        sub = np.concatenate([data[int(off[i]):int(off[i + 1])] for i in idx])
+        so = np.zeros(idx.size + 1, dtype=np.uint64)
+        so[1:] = np.cumsum(sub_lens)
+        vw = o.hash_var(sub, so)
+        ok = ok and np.array_equal(vout[idx], vw) and np.array_equal(vpo.numpy().view(np.uint64)[idx], vw)
+        res["verified"] = bool(ok)
+    except Exception as e:  # noqa: BLE001
+        res["verified"] = None
+        res["verify_note"] = "oracle unavailable: %s" % e
+    res["var_mean_key_bytes"] = float(off[-1]) / n
     return res
 
 
 # ---------------------------------------------------------------------------
 # CPU baseline: the reference's own shf_make_hash() loop (test.9 shape)
 # ---------------------------------------------------------------------------
+def host_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2
+    cpu.max quota when there is one."""
+    vis = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = vis
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return {"visible": vis, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(args):
     from sharedhashfile_amd.keygen import splitmix_bytes
 
@@ -279,186 +516,307 @@ def cpu_baseline(args):
         ref = None
     import ctypes
 
-    if ref is not None:
-        fold = ctypes.c_uint64(0)
-        dt1 = ref.ref_bench_make_hash_loop(keys.ctypes.data, L, n, 1, 1, ctypes.byref(fold))
-        passes = max(1, int(args.cpu_seconds / max(dt1, 1e-6)))
-        dt = ref.ref_bench_make_hash_loop(keys.ctypes.data, L, n, passes, 1, ctypes.byref(fold))
-        kind = "reference"
-        what = "oracle/_ref/libref_shf.so: reference src/shf.c shf_make_hash() + src/murmurhash3.c, gcc -O2"
-    else:
+    fold = ctypes.c_uint64(0)
+    o = None
+    if ref is None:
         from oracle.oracle_py import Oracle
 
         o = Oracle()
-        t0 = time.perf_counter()
-        o.hash_fixed(keys, L)
-        dt1 = time.perf_counter() - t0
-        passes = max(1, int(args.cpu_seconds / max(dt1, 1e-6)))
+
+    def run(passes, threads):
+        if ref is not None:
+            return ref.ref_bench_make_hash_loop(keys.ctypes.data, L, n, passes, threads, ctypes.byref(fold))
         t0 = time.perf_counter()
         for _ in range(passes):
-            o.hash_fixed(keys, L)
-        dt = time.perf_counter() - t0
-        kind = "port"
-        what = "oracle/murmur3_oracle.c restatement, gcc -O2"
+            o.hash_fixed(keys, L, threads=threads)
+        return time.perf_counter() - t0
+
+    if ref is not None:
+        kind, what = "reference", "oracle/_ref/libref_shf.so: reference src/shf.c shf_make_hash() + src/murmurhash3.c, gcc -O2"
+    else:
+        kind, what = "port", "oracle/murmur3_oracle.c restatement, gcc -O2"
+    dt1 = run(1, 1)
+    passes = max(1, int(args.cpu_seconds / max(dt1, 1e-6)))
+    dt = run(passes, 1)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
-    out = {"value": n * passes / dt, "unit": "keys/s", "cores": 1, "kind": kind,
-           "sample": "%d passes x 1M 16-B keys (test.9 loop shape, hash only), %.1f s, %s; host %s (%d cpus visible)"
-                     % (passes, dt, what, model, os.cpu_count() or 0)}
-    # SURVEY.md s8(d) config A also asks for all cores: the box's CPU share for one GPU is 16 threads
-    threads = args.cpu_threads
+    cpus = host_cpus()
+    one = n * passes / dt
+    out = {"value": one, "unit": "keys/s", "cores": 1, "kind": kind,
+           "sample": "%d passes x 1M 16-B keys (test.9 loop shape, hash only), %.1f s, one thread, %s; host %s"
+                     % (passes, dt, what, model),
+           "host_cpus": cpus}
+    # SURVEY.md s8(d) config A also asks for the host's cores. This box's rule
+    # sizes host worker pools to its CPU share per GPU (16 threads): that leg is
+    # measured; the whole host (`visible` CPUs) is extrapolated from the
+    # per-thread rate of that leg, never measured here, and labelled so.
+    threads = min(BOX_CPU_SHARE, cpus["affinity"])
     if threads > 1:
-        mt_passes = max(1, int(passes * threads / 4))  # ~1/4 of the single-core time if it scales
-        if ref is not None:
-            dt_mt = ref.ref_bench_make_hash_loop(keys.ctypes.data, L, n, mt_passes, threads, ctypes.byref(fold))
-        else:
-            t0 = time.perf_counter()
-            for _ in range(mt_passes):
-                o.hash_fixed(keys, L, threads=threads)
-            dt_mt = time.perf_counter() - t0
-        out["all_cores"] = {"value": n * mt_passes / dt_mt, "unit": "keys/s", "cores": threads,
-                            "sample": "%d passes x 1M 16-B keys over %d threads (even key ranges), %.1f s"
-                                      % (mt_passes, threads, dt_mt)}
+        mt_passes = max(1, int(passes * threads / 4))  # ~1/4 of the single-thread time if it scales
+        dt_mt = run(mt_passes, threads)
+        v = n * mt_passes / dt_mt
+        out["threads%d" % threads] = {"value": v, "unit": "keys/s", "cores": threads,
+                                      "sample": "%d passes x 1M 16-B keys over %d threads (even key ranges), %.1f s"
+                                                % (mt_passes, threads, dt_mt)}
+        out["all_visible_cpus_extrapolated"] = {
+            "value": v / threads * cpus["visible"], "unit": "keys/s", "cores": cpus["visible"], "measured": False,
+            "sample": "the %d-thread rate per thread x %d visible CPUs (linear scaling assumed; not run: the GPU box "
+                      "limits a job's host worker pools to its %d-CPU share)" % (threads, cpus["visible"],
+                                                                                BOX_CPU_SHARE)}
     return out
 
 
 # ---------------------------------------------------------------------------
-# HBM traffic from rocprofv3 PMC counters (child processes, N=1 only)
+# rocprofv3 PMC passes (child processes, N=1 only): HBM bytes and VALU busy
 # ---------------------------------------------------------------------------
-def collect_traffic(args, kernel_sym):
-    """Two --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950).
-    Per MI355X_MICROARCH.md s HBM: FETCH_SIZE reads half the bytes of a wide
-    coalesced stream on gfx950 -> doubled; both are in KiB."""
+PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"],
+              ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"]]
+
+
+def collect_pmc(args, names):
+    """One rocprofv3 --pmc pass per counter group over a short child bench of
+    the given workloads (the 16-B workloads at the headline size; configs 2
+    and 3 at 10M keys, whose per-key figures do not depend on the batch size).
+    Returns ({workload: {counter: median per launch}}, note)."""
     prof = shutil.which("rocprofv3")
     if not prof:
         return None, "rocprofv3 not found"
-    res = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    want = [x for x in names if x in KERNEL_SYMS and x not in ("fixed16_hot", "shard1b")]
+    res = {w: {} for w in want}
+    for group in PMC_PASSES:
         outdir = tempfile.mkdtemp(prefix="shfhb_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
-               sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--only", "fixed16",
-               "--no-cpu", "--traffic", "off", "--quiet", "--keys16", str(args.keys16), "--warmup-min-s", "0"]
+        cmd = [prof, "--pmc"] + group + ["--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
+                                         sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup",
+                                         "1", "--repeats", "1", "--only", ",".join(want), "--no-cpu", "--no-verify",
+                                         "--no-host-inclusive", "--traffic", "off", "--quiet", "--keys16",
+                                         str(args.keys16), "--keys256", str(min(args.keys256, 10_000_000)),
+                                         "--keysvar", str(min(args.keysvar, 10_000_000)), "--warmup-min-s", "0",
+                                         "--gpus", "1"]
         try:
             subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            cwd=os.environ.get("TMPDIR", "/tmp"))
         except Exception as e:  # noqa: BLE001
-            return None, "rocprofv3 %s pass failed: %s" % (counter, e)
-        vals = []
+            shutil.rmtree(outdir, ignore_errors=True)
+            return None, "rocprofv3 --pmc %s failed: %s" % (" ".join(group), e)
+        vals = {}
         for f in glob.glob(os.path.join(outdir, "**", "*counter_collection*.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if kernel_sym in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                        vals.append(float(row["Counter_Value"]))
+                    for w in want:
+                        if KERNEL_SYMS[w] in row.get("Kernel_Name", ""):
+                            vals.setdefault((w, row.get("Counter_Name")), []).append(float(row["Counter_Value"]))
         shutil.rmtree(outdir, ignore_errors=True)
-        if not vals:
-            return None, "no %s rows for %s" % (counter, kernel_sym)
-        res[counter] = float(np.median(vals))
-    fetch = 2.0 * res["FETCH_SIZE"] * 1024.0
-    write = res["WRITE_SIZE"] * 1024.0
-    return fetch + write, "per launch: 2 x FETCH_SIZE (%.0f KiB) + WRITE_SIZE (%.0f KiB), median of 3 launches" % (
-        res["FETCH_SIZE"], res["WRITE_SIZE"])
+        for (w, c), v in vals.items():
+            res[w][c] = float(np.median(v))
+    return res, ("per launch, median over the child's launches; FETCH_SIZE doubled (gfx950 reports half the "
+                 "bytes of a wide coalesced read, MI355X_MICROARCH.md) + WRITE_SIZE, both KiB; valu_busy = "
+                 "4 x SQ_ACTIVE_INST_VALU / (%d SIMDs x GRBM_GUI_ACTIVE / %d XCDs) (rocprof's VALUBusy formula, "
+                 "SQ_ACTIVE_INST_* in quad-cycles); configs 2/3 measured at <= 10M keys" % (SIMDS, XCDS))
 
 
-def main():
-    args = parse()
-    rank, world, local = dist_env()
+def pmc_fields(c, algorithmic_bytes):
+    out = {}
+    if c.get("FETCH_SIZE") is not None and c.get("WRITE_SIZE") is not None:
+        t = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        out["traffic"] = t
+        out["traffic_over_algorithmic"] = round(t / algorithmic_bytes, 4) if algorithmic_bytes else None
+    if c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
+        out["valu_busy"] = round(4.0 * c["SQ_ACTIVE_INST_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS), 4)
+    return out
+
+
+def limiter(achieved_gbs, valu_busy):
+    """Which resource is closer to its ceiling: the HBM (against the measured
+    copy ceiling) or the VALU."""
+    h = achieved_gbs / HBM_COPY_GBS
+    if valu_busy is None:
+        return "hbm (valu not measured)"
+    return "hbm" if h >= valu_busy else "valu"
+
+
+# ---------------------------------------------------------------------------
+def summarize(w, walls, devs, steps, keys_total):
+    vals = [keys_total / t for t in walls]
+    i_med = int(np.argsort(vals)[len(vals) // 2])
+    per_launch = devs[i_med]
+    return {
+        "value": vals[i_med],
+        "value_min": min(vals), "value_max": max(vals), "repeats": len(vals),
+        "ms_per_step": 1e3 * walls[i_med] / steps,
+        "kernel_us": per_launch * 1e6,
+        "achieved_gbs": w.n * w.bytes_per_key / per_launch / 1e9,
+        "bytes_per_key": w.bytes_per_key,
+        "kernel": w.kernel,
+        "desc": w.desc,
+        "enqueue_us_per_step": 1e6 * w.enqueue_s / steps,
+    }
+
+
+def run_rank(args):
+    rank, world, local, local_world = dist_env()
     import torch
 
     import sharedhashfile_amd as hb
 
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU (HIP); none visible")
-    local = local % max(1, torch.cuda.device_count())  # ranks beyond the visible GPUs share them (rehearsal)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
+    dev_idx, shared = plan_device(local, local_world, torch.cuda.device_count(), args.allow_shared_gpu)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    dist, dist_dev = None, "cpu"
     if world > 1:
         import torch.distributed as tdist
 
-        if args.dist_backend == "nccl":  # RCCL: barriers + one max-reduce, no data path
+        backend = args.dist_backend
+        if backend == "auto":
+            backend = "gloo" if shared else "nccl"
+        if backend == "nccl":  # RCCL: barriers + max-reduces, no data path
+            if shared:
+                raise SystemExit("bench.py: RCCL cannot run two ranks on one GPU; use --dist-backend gloo")
             tdist.init_process_group("nccl", device_id=dev)
+            dist_dev = dev
         else:
             tdist.init_process_group("gloo")
         dist = tdist
     hb.check_device()
+    n_gpus = min(world, torch.cuda.device_count()) if shared else world
 
     wl = make_workloads(args, dev, rank, world)
     results = {}
+    verified = {}
     for w in wl:
-        elapsed, per_launch = time_workload(w, args.steps, args.warmup, dist, args.warmup_min_s)
-        keys_total = getattr(w, "job_keys", w.n * world) * args.steps
-        results[w.name] = {
-            "value": keys_total / elapsed,
-            "ms_per_step": 1e3 * elapsed / args.steps,
-            "kernel_us": per_launch * 1e6,
-            "achieved_gbs": w.n * w.bytes_per_key / per_launch / 1e9,
-            "bytes_per_key": w.bytes_per_key,
-            "kernel": w.kernel,
-            "desc": w.desc,
-            "enqueue_us_per_step": 1e6 * w.enqueue_s / args.steps,
-        }
-        log(args, "[bench] %s: %.3f Gkeys/s, %.1f us/launch, %.0f GB/s, host enqueue %.1f us/step" % (
-            w.name, results[w.name]["value"] / 1e9, per_launch * 1e6, results[w.name]["achieved_gbs"],
-            1e6 * w.enqueue_s / args.steps))
+        walls, devs = time_workload(w, args.steps, args.warmup, args.repeats, dist, dist_dev, args.warmup_min_s)
+        keys_total = (w.job_keys or w.n * world) * args.steps
+        r = results[w.name] = summarize(w, walls, devs, args.steps, keys_total)
+        log(args, "[bench] %s: %.3f Gkeys/s (min %.3f, max %.3f), %.1f us/launch, %.0f GB/s, enqueue %.1f us/step"
+            % (w.name, r["value"] / 1e9, r["value_min"] / 1e9, r["value_max"] / 1e9, r["kernel_us"],
+               r["achieved_gbs"], r["enqueue_us_per_step"]))
+        if not args.no_verify and w.verify is not None:
+            try:
+                ok, checked = w.verify()
+            except Exception as e:  # noqa: BLE001
+                ok, checked = None, 0
+                log(args, "[bench] %s: verify unavailable: %s" % (w.name, e))
+            if dist:
+                t = torch.tensor([1 if ok else (0 if ok is False else -1)], dtype=torch.int64, device=dist_dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                ok = True if int(t[0]) == 1 else (False if int(t[0]) == 0 else None)
+            verified[w.name] = {"ok": ok, "samples_per_rank": checked}
+            if ok is False:
+                raise SystemExit("bench.py: %s outputs differ from the oracle" % w.name)
+    shards = None
+    sw = next((w for w in wl if w.name == "shard1b"), None)
+    if sw is not None and dist:
+        t = torch.zeros(2 * world, dtype=torch.int64, device=dist_dev)
+        t[2 * rank], t[2 * rank + 1] = sw.shard[0], sw.shard[1]
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        shards = [[int(t[2 * r]), int(t[2 * r + 1])] for r in range(world)]
+    elif sw is not None:
+        shards = [list(sw.shard)]
 
     if rank == 0:
-        head = results.get("fixed16") or next(iter(results.values()))
-        traffic, traffic_note = None, "not collected"
-        if world == 1 and args.traffic == "auto" and "fixed16" in results:
-            traffic, traffic_note = collect_traffic(args, "k_fixed16")
-        roof = {"bound": "hbm", "achieved": round(head["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(head["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": head["kernel"], "kernel_us": round(head["kernel_us"], 2),
-                "algorithmic_bytes_per_launch": int(args.keys16 * 32) if "fixed16" in results else None,
-                "traffic_note": traffic_note}
+        pmc, pmc_note = None, "not collected"
+        if world == 1 and args.traffic == "auto":
+            pmc, pmc_note = collect_pmc(args, list(results))
+        head_name = "fixed16" if "fixed16" in results else next(iter(results))
+        head = results[head_name]
+
+        def roofline(name, r):
+            ro = {"bound": "hbm", "achieved": round(r["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                  "frac_of_copy_ceiling": round(r["achieved_gbs"] / HBM_COPY_GBS, 4),
+                  "bytes_per_key": round(r["bytes_per_key"], 2), "kernel": r["kernel"],
+                  "kernel_us": round(r["kernel_us"], 2)}
+            c = (pmc or {}).get(name if name not in ("fixed16_hot", "shard1b") else "fixed16")
+            if c:
+                # keys per launch in the PMC child (configs 2/3 run there at <= 10M keys)
+                pk = {"fixed256": min(args.keys256, 10_000_000), "var": min(args.keysvar, 10_000_000)}.get(
+                    name, args.keys16)
+                f = pmc_fields(c, pk * r["bytes_per_key"])
+                if name in ("fixed16", "fixed16_hot", "probe16"):
+                    ro["traffic"] = f.get("traffic")
+                else:
+                    ro["traffic_at_pmc_size"] = f.get("traffic")
+                ro["traffic_over_algorithmic"] = f.get("traffic_over_algorithmic")
+                ro["valu_busy"] = f.get("valu_busy")
+            ro["limiter"] = limiter(r["achieved_gbs"], ro.get("valu_busy"))
+            return ro
+
+        roof = roofline(head_name, head)
+        roof["algorithmic_bytes_per_launch"] = int(head["bytes_per_key"] * args.keys16) if head_name == "fixed16" \
+            else None
+        roof["traffic_note"] = pmc_note
+        secondary = {}
+        for name, r in results.items():
+            if name == head_name:
+                continue
+            secondary[name] = {"value": r["value"], "value_min": r["value_min"], "value_max": r["value_max"],
+                               "unit": "keys/s", "ms_per_step": round(r["ms_per_step"], 4), "desc": r["desc"],
+                               "roofline": roofline(name, r), "verified": verified.get(name)}
+            if name == "shard1b":
+                secondary[name]["scaling"] = "strong"
+                secondary[name]["shards"] = shards
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(args)
-        secondary = {}
-        for name, r in results.items():
-            if name == "fixed16":
-                continue
-            secondary[name] = {"value": r["value"], "unit": "keys/s", "ms_per_step": round(r["ms_per_step"], 4),
-                               "desc": r["desc"], "kernel": r["kernel"], "kernel_us": round(r["kernel_us"], 2),
-                               "roofline": {"bound": "hbm", "achieved": round(r["achieved_gbs"], 1),
-                                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                            "frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                                            "bytes_per_key": round(r["bytes_per_key"], 2)}}
-            if name == "shard1b":
-                secondary[name]["scaling"] = "strong"
+        host_inc = None
+        if world == 1 and not args.no_host_inclusive:
+            host_inc = time_host_inclusive(args, dev)
+        all_ok = all(v["ok"] is True for v in verified.values()) if verified else None
         line = {
             "metric": METRIC,
             "value": head["value"],
             "unit": "keys/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "repeats": args.repeats,
+            "value_min": head["value_min"],
+            "value_max": head["value_max"],
             "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic: random key bytes generated on device (torch Philox), resident in HBM before timing",
-            "config": {"workload": "BASELINE configs[1]: %d fixed 16-B keys per GPU, MurmurHash3_x64_128 seed "
-                                   "12345 -> 16-B SHF_HASH (shf_make_hash batch)" % args.keys16,
+            "config": {"workload": "BASELINE configs[1]: %d fixed 16-B keys per GPU per step, MurmurHash3_x64_128 "
+                                   "seed 12345 -> 16-B SHF_HASH (shf_make_hash batch), rotating over %d distinct "
+                                   "batches" % (args.keys16, max(1, args.rotate)),
                        "keys_per_gpu": args.keys16, "key_len": 16,
-                       "parallelism": "dp%d (independent key shards, no collective)" % world},
+                       "parallelism": "dp%d (independent key shards, no collective)" % n_gpus},
             "roofline": roof,
+            "verified": all_ok,
+            "verification": verified,
             "cpu_baseline": cpu,
+            "host_inclusive": host_inc,
             "secondary": secondary,
         }
-        if args.host_inclusive and world == 1:
-            line["host_inclusive"] = time_host_inclusive(args)
+        if shared:
+            line["rehearsal"] = True
+            line["rehearsal_note"] = "%d ranks shared %d GPU(s) (--allow-shared-gpu): throughput is not a " \
+                                     "multi-GPU measurement" % (world, n_gpus)
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = args.gpus or 1
+        if n > 1:  # spawn the ranks before anything touches the GPU
+            return launch_ranks(argv, n)
+    elif args.gpus is not None and args.gpus != int(env_world):
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, env_world))
+    run_rank(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

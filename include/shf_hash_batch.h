@@ -33,7 +33,14 @@
  *     current HIP device (hipSetDevice), as HIP itself does.
  *   - Key lengths follow the reference's `const int len` parameter
  *     (murmurhash3.c:75): key_len and every variable key length must be
- *     < 2^31, else SHF_HB_ERR_ARG.
+ *     < 2^31, else SHF_HB_ERR_ARG. A variable-length key is invalid when its
+ *     offsets decrease (offsets[i+1] < offsets[i]) or span 2^31 bytes or more.
+ *     Host-memory calls check the offsets before any transfer. Device-resident
+ *     offsets are checked by the kernels: an invalid key's bytes are never
+ *     read and its output record is left unwritten (every valid key of the
+ *     batch is still hashed); the synchronous calls then return
+ *     SHF_HB_ERR_ARG, and the asynchronous ones report it through
+ *     shf_hash_batch_status().
  */
 #ifndef SHF_HASH_BATCH_H
 #define SHF_HASH_BATCH_H
@@ -224,6 +231,14 @@ SHF_HB_API int shf_probe_batch_fixed_kernel_async(const shf_row_index *index, co
                                                   uint32_t key_len, uint64_t n, uint32_t seed,
                                                   shf_hash128 *d_hashes, shf_probe *d_probe, int kernel,
                                                   void *hip_stream);
+
+/* ---- status of asynchronous variable-length calls -------------------------
+ * Waits for hip_stream (NULL = the null stream), then returns SHF_HB_ERR_ARG if
+ * any asynchronous variable-length call (hashing, UID parts or probe) that
+ * this thread enqueued on its current device since the previous query met an
+ * invalid key (see Conventions), else SHF_HB_OK; the query clears the flag.
+ * Calls still running on other streams are reported by a later query. */
+SHF_HB_API int shf_hash_batch_status(void *hip_stream);
 
 /* ---- info ----------------------------------------------------------------- */
 SHF_HB_API int shf_hash_batch_device_count(void);          /* visible HIP devices, or a negative status */

@@ -89,6 +89,7 @@ _SIGS = {
     "shf_probe_batch_fixed": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _INT],
     "shf_probe_batch_var": [_VP, _VP, _VP, _U64, _U32, _VP, _VP, _INT],
     "shf_probe_batch_fixed_kernel_async": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _INT, _VP],
+    "shf_hash_batch_status": [_VP],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
@@ -142,13 +143,59 @@ def _stream_handle(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def _require_cuda_u8(t, name):
+def _require_cuda(t, name, dtypes):
     import torch
 
     if not (isinstance(t, torch.Tensor) and t.is_cuda):
         raise TypeError("%s must be a CUDA (HIP) tensor" % name)
+    if t.dtype not in dtypes:
+        raise TypeError("%s must be %s, not %s" % (name, " or ".join(str(d) for d in dtypes), t.dtype))
     if not t.is_contiguous():
         raise ValueError("%s must be contiguous" % name)
+
+
+def _require_cuda_u8(t, name):
+    import torch
+
+    _require_cuda(t, name, (torch.uint8,))
+
+
+def _offset_dtypes():
+    import torch
+
+    return tuple(d for d in (torch.int64, getattr(torch, "uint64", None)) if d is not None)
+
+
+def _require_offsets(offsets, data):
+    """offsets: contiguous 1-D int64/uint64 CUDA tensor of n + 1 >= 1 entries on data's device."""
+    _require_cuda(offsets, "offsets", _offset_dtypes())
+    if offsets.dim() != 1 or offsets.numel() < 1:
+        raise ValueError("offsets must be 1-D with n + 1 >= 1 entries")
+    if offsets.device != data.device:
+        raise ValueError("offsets (%s) and data (%s) must be on the same GPU" % (offsets.device, data.device))
+    return offsets.numel() - 1
+
+
+def _require_out(out, shape, dtypes, device):
+    _require_cuda(out, "out", dtypes)
+    if tuple(out.shape) != tuple(shape):
+        raise ValueError("out must have shape %s, not %s" % (tuple(shape), tuple(out.shape)))
+    if out.device != device:
+        raise ValueError("out (%s) must be on %s" % (out.device, device))
+
+
+def _on(t):
+    """The device context of tensor t: the library runs on the calling thread's
+    current device and stream, so every call is made on t's device."""
+    import torch
+
+    return torch.cuda.device(t.device)
+
+
+def status(stream=None):
+    """shf_hash_batch_status(): raises ShfHashBatchError(ERR_ARG) if an async
+    variable-length call of this thread met an invalid key since the last query."""
+    _check(load().shf_hash_batch_status(_stream_handle(stream)), "shf_hash_batch_status")
 
 
 def hash_fixed(keys, key_len=None, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO):
@@ -169,9 +216,11 @@ def hash_fixed(keys, key_len=None, seed=SEED, out=None, stream=None, kernel=KERN
         n = keys.numel() // key_len if key_len else 0
     if out is None:
         out = torch.empty((n, 2), dtype=torch.int64, device=keys.device)
-    rc = load().shf_hash_batch_fixed_kernel_async(
-        ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()), kernel,
-        _stream_handle(stream))
+    _require_out(out, (n, 2), (torch.int64,), keys.device)
+    with _on(keys):
+        rc = load().shf_hash_batch_fixed_kernel_async(
+            ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()), kernel,
+            _stream_handle(stream))
     _check(rc, "shf_hash_batch_fixed_kernel_async")
     return out
 
@@ -186,18 +235,20 @@ def hash_var(data, offsets, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO
     import torch
 
     _require_cuda_u8(data, "data")
-    n = offsets.numel() - 1
+    n = _require_offsets(offsets, data)
     if out is None:
-        out = torch.empty((max(n, 0), 2), dtype=torch.int64, device=data.device)
-    if key_bytes is None:
-        rc = load().shf_hash_batch_var_kernel_async(
-            ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
+        out = torch.empty((n, 2), dtype=torch.int64, device=data.device)
+    _require_out(out, (n, 2), (torch.int64,), data.device)
+    with _on(data):
+        if key_bytes is None:
+            rc = load().shf_hash_batch_var_kernel_async(
+                ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
+                ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
+            _check(rc, "shf_hash_batch_var_kernel_async")
+            return out
+        rc = load().shf_hash_batch_var_sized_kernel_async(
+            ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, int(key_bytes), seed,
             ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
-        _check(rc, "shf_hash_batch_var_kernel_async")
-        return out
-    rc = load().shf_hash_batch_var_sized_kernel_async(
-        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), int(key_bytes), seed,
-        ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
     _check(rc, "shf_hash_batch_var_sized_kernel_async")
     return out
 
@@ -213,8 +264,11 @@ def uid_parts_fixed(keys, key_len=None, seed=SEED, out=None, stream=None):
         n = keys.numel() // key_len if key_len else 0
     if out is None:
         out = torch.empty((n,), dtype=torch.int64, device=keys.device)
-    rc = load().shf_uid_parts_batch_fixed_async(
-        ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _require_out(out, (n,), (torch.int64,), keys.device)
+    with _on(keys):
+        rc = load().shf_uid_parts_batch_fixed_async(
+            ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()),
+            _stream_handle(stream))
     _check(rc, "shf_uid_parts_batch_fixed_async")
     return out
 
@@ -223,12 +277,14 @@ def uid_parts_var(data, offsets, seed=SEED, out=None, stream=None):
     import torch
 
     _require_cuda_u8(data, "data")
-    n = offsets.numel() - 1
+    n = _require_offsets(offsets, data)
     if out is None:
-        out = torch.empty((max(n, 0),), dtype=torch.int64, device=data.device)
-    rc = load().shf_uid_parts_batch_var_async(
-        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), max(n, 0), seed,
-        ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+        out = torch.empty((n,), dtype=torch.int64, device=data.device)
+    _require_out(out, (n,), (torch.int64,), data.device)
+    with _on(data):
+        rc = load().shf_uid_parts_batch_var_async(
+            ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
+            ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_uid_parts_batch_var_async")
     return out
 
@@ -334,11 +390,13 @@ def probe_fixed(index, keys, key_len=None, seed=SEED, out=None, hashes=False, st
         n = keys.numel() // key_len if key_len else 0
     if out is None:
         out = torch.empty((n, 4), dtype=torch.int32, device=keys.device)
+    _require_out(out, (n, 4), (torch.int32,), keys.device)
     hout = torch.empty((n, 2), dtype=torch.int64, device=keys.device) if hashes else None
-    rc = load().shf_probe_batch_fixed_kernel_async(
-        index.handle, ctypes.c_void_p(keys.data_ptr()), key_len, n, seed,
-        ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()), kernel,
-        _stream_handle(stream))
+    with _on(keys):
+        rc = load().shf_probe_batch_fixed_kernel_async(
+            index.handle, ctypes.c_void_p(keys.data_ptr()), key_len, n, seed,
+            ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()), kernel,
+            _stream_handle(stream))
     _check(rc, "shf_probe_batch_fixed_kernel_async")
     return (out, hout) if hashes else out
 
@@ -347,14 +405,16 @@ def probe_var(index, data, offsets, seed=SEED, out=None, hashes=False, stream=No
     import torch
 
     _require_cuda_u8(data, "data")
-    n = max(offsets.numel() - 1, 0)
+    n = _require_offsets(offsets, data)
     if out is None:
         out = torch.empty((n, 4), dtype=torch.int32, device=data.device)
+    _require_out(out, (n, 4), (torch.int32,), data.device)
     hout = torch.empty((n, 2), dtype=torch.int64, device=data.device) if hashes else None
-    rc = load().shf_probe_batch_var_async(
-        index.handle, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
-        ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()),
-        _stream_handle(stream))
+    with _on(data):
+        rc = load().shf_probe_batch_var_async(
+            index.handle, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
+            ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()),
+            _stream_handle(stream))
     _check(rc, "shf_probe_batch_var_async")
     return (out, hout) if hashes else out
 
@@ -363,13 +423,16 @@ def probe_hashes(index, hashes, out=None, stream=None):
     """Row pre-probe of precomputed (n, 2) int64 CUDA hashes."""
     import torch
 
-    if not (isinstance(hashes, torch.Tensor) and hashes.is_cuda and hashes.is_contiguous()):
-        raise TypeError("hashes must be a contiguous CUDA tensor")
+    _require_cuda(hashes, "hashes", _offset_dtypes())
+    if hashes.dim() != 2 or hashes.shape[1] != 2:
+        raise ValueError("hashes must have shape (n, 2)")
     n = hashes.shape[0]
     if out is None:
         out = torch.empty((n, 4), dtype=torch.int32, device=hashes.device)
-    rc = load().shf_probe_batch_hashes_async(index.handle, ctypes.c_void_p(hashes.data_ptr()), n,
-                                             ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _require_out(out, (n, 4), (torch.int32,), hashes.device)
+    with _on(hashes):
+        rc = load().shf_probe_batch_hashes_async(index.handle, ctypes.c_void_p(hashes.data_ptr()), n,
+                                                 ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_probe_batch_hashes_async")
     return out
 

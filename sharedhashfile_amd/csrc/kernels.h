@@ -26,6 +26,7 @@ struct Sink {
   const uint32_t* tab_slot = nullptr;  // kOutProbe: row index, see shf_hash_batch.h
   const uint8_t* rows = nullptr;
   uint64_t n_slots = 0;
+  uint32_t* status = nullptr;  // variable-length keys: set to 1 when a key's offsets are invalid
 };
 
 // keys: device pointer to n * key_len bytes.

@@ -202,6 +202,18 @@ __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Variable-length key check (include/shf_hash_batch.h: every key length must be
+// < 2^31, the reference's `const int len`, murmurhash3.c:75). A key whose
+// offsets decrease or span 2^31 bytes or more is skipped -- its bytes are never
+// read, its record never written -- and the call's status word is set.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool var_key_bad(uint64_t o0, uint64_t o1) { return o1 < o0 || o1 - o0 > 0x7fffffffull; }
+
+__device__ __forceinline__ void flag_bad_key(const Sink& sink) {
+  if (sink.status) *reinterpret_cast<volatile uint32_t*>(sink.status) = 1u;
+}
+
+// ---------------------------------------------------------------------------
 // key_len == 16
 // ---------------------------------------------------------------------------
 // One key per lane and as many workgroups as keys need: no grid-stride loop
@@ -356,6 +368,10 @@ __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ byt
     uint32_t len;
     if constexpr (VAR) {
       const uint64_t o0 = offsets[i], o1 = offsets[i + 1];
+      if (var_key_bad(o0, o1)) {
+        flag_bad_key(sink);
+        continue;
+      }
       start = o0 - off_base;
       len = (uint32_t)(o1 - o0);
     } else {
@@ -828,13 +844,20 @@ __global__ __launch_bounds__(64) void k_vround(const uint8_t* __restrict__ bytes
                                                uint64_t off_base, uint64_t n, uint32_t seed, Sink sink) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kVrLdsBytes];
   const uint64_t key = (uint64_t)blockIdx.x * 64u + threadIdx.x;
-  const bool valid = key < n;
+  bool valid = key < n;
   uint64_t start = 0;
   uint32_t len = 0;
+  bool bad = false;
   if (valid) {
     const uint64_t o0 = offsets[key], o1 = offsets[key + 1];
+    bad = var_key_bad(o0, o1);
     start = o0 - off_base;
     len = (uint32_t)(o1 - o0);
+  }
+  if (__ballot(bad)) {  // wave-uniform: the tile's span is not trustworthy; per-lane hashing of its good keys
+    if (bad) flag_bad_key(sink);
+    else if (valid) store_result<OUT>(sink, key, hash_bytes(bytes + start, len, seed));
+    return;
   }
   vround_tile<OUT>(bytes, key, valid, start, len, seed, sink, lds);
 }
@@ -848,8 +871,17 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
                                              uint32_t cap, Sink sink) {
   extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
   const uint32_t lane = threadIdx.x;
-  const SpanTile<VAR> ti =
-      span_finish<VAR>(bytes, off_base, key_len, n, span_load<VAR>(offsets, n, blockIdx.x, lane), lane);
+  const SpanRaw raw = span_load<VAR>(offsets, n, blockIdx.x, lane);
+  if constexpr (VAR) {
+    const bool bad = var_key_bad(raw.o0, raw.o1);  // lanes past n carry o0 = o1 = 0
+    if (__ballot(bad)) {  // wave-uniform: no span for this tile; per-lane hashing of its good keys
+      const uint64_t key = raw.t * 64u + lane;
+      if (bad) flag_bad_key(sink);
+      else if (key < n) store_result<OUT>(sink, key, hash_bytes(bytes + (raw.o0 - off_base), (uint32_t)(raw.o1 - raw.o0), seed));
+      return;
+    }
+  }
+  const SpanTile<VAR> ti = span_finish<VAR>(bytes, off_base, key_len, n, raw, lane);
   if (ti.span16 <= cap) {
     u32x4 reg[PIECES];
     span_fetch<PIECES>(reg, ti.base, ti.span16, lane);

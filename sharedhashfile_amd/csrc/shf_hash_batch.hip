@@ -11,8 +11,15 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -98,9 +105,28 @@ struct DevCtx {
   shf_probe* d_probe[kMaxSlots] = {};
   size_t probe_cap = 0;
   int n_staged = 0;  // slots whose staging buffers are allocated
+  // Variable-length key checks done by the kernels (kernels.h Sink::status):
+  // word 0 collects this thread's async calls until shf_hash_batch_status()
+  // reads it, word 1 is cleared and read by each synchronous call.
+  uint32_t* d_status = nullptr;
+  uint32_t* h_status = nullptr;  // pinned, 1 word
 };
 
-thread_local std::map<int, DevCtx*> tls_ctx;
+void release_ctx(DevCtx* c);
+
+// The calling thread's contexts, one per device, freed when the thread exits
+// (streams, events, pinned and device staging). Not on the main thread at
+// process exit: the HIP runtime may already be going away, and the process's
+// memory goes with it anyway.
+struct ThreadCtxs {
+  std::map<int, DevCtx*> m;
+  ~ThreadCtxs() {
+    if ((pid_t)syscall(SYS_gettid) == getpid()) return;
+    for (auto& kv : m) release_ctx(kv.second);
+    m.clear();
+  }
+};
+thread_local ThreadCtxs tls_ctx;
 
 int check_arch(int dev) {
   hipDeviceProp_t p;
@@ -116,8 +142,8 @@ int current_ctx(DevCtx** out) {
     (void)hipGetLastError();
     return map_hip(e) == SHF_HB_ERR_HIP ? SHF_HB_ERR_NODEV : map_hip(e);
   }
-  auto it = tls_ctx.find(dev);
-  if (it != tls_ctx.end()) {
+  auto it = tls_ctx.m.find(dev);
+  if (it != tls_ctx.m.end()) {
     *out = it->second;
     return it->second->status;
   }
@@ -129,8 +155,12 @@ int current_ctx(DevCtx** out) {
       c->status = map_hip(hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking));
       if (c->status == SHF_HB_OK) c->status = map_hip(hipEventCreateWithFlags(&c->done[s], hipEventDisableTiming));
     }
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 2 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 2 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK)
+      c->status = map_hip(hipHostMalloc((void**)&c->h_status, sizeof(uint32_t), hipHostMallocDefault));
   }
-  tls_ctx[dev] = c;
+  tls_ctx.m[dev] = c;
   *out = c;
   return c->status;
 }
@@ -154,25 +184,30 @@ void free_staging(DevCtx* c) {
   c->n_staged = 0;
 }
 
-// Release every context of this thread (worker threads of the *_multi calls).
-void release_thread_ctx() {
-  for (auto& kv : tls_ctx) {
-    DevCtx* c = kv.second;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(c->dev);
-    for (int s = 0; s < kMaxSlots; ++s) {
-      if (c->st[s]) (void)hipStreamSynchronize(c->st[s]);
-    }
-    free_staging(c);
-    for (int s = 0; s < kMaxSlots; ++s) {
-      if (c->done[s]) (void)hipEventDestroy(c->done[s]);
-      if (c->st[s]) (void)hipStreamDestroy(c->st[s]);
-    }
-    (void)hipSetDevice(prev);
-    delete c;
+void release_ctx(DevCtx* c) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(c->dev);
+  for (int s = 0; s < kMaxSlots; ++s) {
+    if (c->st[s]) (void)hipStreamSynchronize(c->st[s]);
   }
-  tls_ctx.clear();
+  free_staging(c);
+  for (int s = 0; s < kMaxSlots; ++s) {
+    if (c->done[s]) (void)hipEventDestroy(c->done[s]);
+    if (c->st[s]) (void)hipStreamDestroy(c->st[s]);
+  }
+  if (c->d_status) (void)hipFree(c->d_status);
+  if (c->h_status) (void)hipHostFree(c->h_status);
+  (void)hipGetLastError();
+  (void)hipSetDevice(prev);
+  delete c;
+}
+
+// Release every context of this thread now (the *_multi workers, before they
+// report back; other threads are covered by ThreadCtxs at thread exit).
+void release_thread_ctx() {
+  for (auto& kv : tls_ctx.m) release_ctx(kv.second);
+  tls_ctx.m.clear();
 }
 
 int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys, int slots) {
@@ -233,6 +268,63 @@ size_t copy_threads() {
   return v >= 1 && v <= 64 ? (size_t)v : 8;
 }
 
+// Persistent staging-copy workers shared by every calling thread: started on
+// first use (up to SHF_HB_COPY_THREADS - 1), never per chunk. Deliberately
+// never destroyed: the workers park on the queue and end with the process.
+class CopyPool {
+ public:
+  void run(const std::vector<std::function<void()>>& pieces) {  // pieces[0] runs on the caller
+    struct Latch {
+      std::mutex m;
+      std::condition_variable cv;
+      size_t left;
+    } latch;
+    latch.left = pieces.size() - 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (workers_ < pieces.size() - 1) {
+        std::thread([this] { work(); }).detach();
+        ++workers_;
+      }
+      for (size_t i = 1; i < pieces.size(); ++i) {
+        const std::function<void()>* f = &pieces[i];
+        q_.push_back([f, &latch] {
+          (*f)();
+          std::lock_guard<std::mutex> l2(latch.m);
+          if (--latch.left == 0) latch.cv.notify_one();
+        });
+      }
+    }
+    cv_.notify_all();
+    pieces[0]();
+    std::unique_lock<std::mutex> lk(latch.m);
+    latch.cv.wait(lk, [&] { return latch.left == 0; });
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  size_t workers_ = 0;
+};
+
+CopyPool& copy_pool() {
+  static CopyPool* p = new CopyPool();
+  return *p;
+}
+
 void par_memcpy(void* dst, const void* src, size_t n) {
   constexpr size_t kMinPerThread = (size_t)2 << 20;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -241,14 +333,13 @@ void par_memcpy(void* dst, const void* src, size_t n) {
     memcpy(dst, src, n);
     return;
   }
-  std::vector<std::thread> th;
   const size_t per = (n + t - 1) / t;
-  for (size_t i = 1; i < t; ++i) {
+  std::vector<std::function<void()>> pieces;
+  for (size_t i = 0; i < t; ++i) {
     const size_t a = i * per, b = std::min(n, a + per);
-    if (a < b) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    if (a < b) pieces.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
   }
-  memcpy(dst, src, std::min(n, per));
-  for (auto& x : th) x.join();
+  copy_pool().run(pieces);
 }
 
 // What a host pipeline writes: hashes and/or row pre-probe records.
@@ -310,11 +401,44 @@ int job_d2h(DevCtx* c, int s, const HostJob& job, uint64_t i0, uint64_t cnt, boo
   return SHF_HB_OK;
 }
 
+// A device buffer for keys larger than the staging (SHF_HB_STAGE_MB): allocated
+// for the one chunk that needs it and freed with it, so the per-slot staging
+// never grows past the stage size.
+struct TmpDevBuf {
+  void* p = nullptr;
+  ~TmpDevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// Fixed-length keys larger than the stage: one key at a time on slot 0,
+// through a temporary device buffer (pageable sources are staged by HIP).
+int host_fixed_big(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
+  int rc = ensure_staging(c, 1, 1, pipeline_slots());
+  if (rc) return rc;
+  if (job.probe && (rc = ensure_probe_staging(c))) return rc;
+  TmpDevBuf tmp;
+  HB_TRY(hipMalloc(&tmp.p, key_len));
+  const bool hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
+  for (uint64_t i = 0; i < n; ++i) {
+    Pending p;
+    HB_TRY(hipMemcpyAsync(tmp.p, keys + i * (uint64_t)key_len, key_len, hipMemcpyHostToDevice, c->st[0]));
+    shfhb::Sink k;
+    int mode = 0;
+    job_sink(c, 0, job, &k, &mode);
+    HB_TRY(shfhb::launch_fixed(tmp.p, key_len, 1, seed, k, mode, c->st[0], shfhb::kKernelAuto));
+    if ((rc = job_d2h(c, 0, job, i, 1, hash_pinned, probe_pinned, &p))) return rc;
+    if ((rc = drain_slot(c, 0, p))) return rc;
+  }
+  return SHF_HB_OK;
+}
+
 // Host-memory fixed-length pipeline on the current device.
 int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
+  if ((uint64_t)key_len > stage_bytes()) return host_fixed_big(c, keys, key_len, n, seed, job);
   const int ns = pipeline_slots();
   const uint64_t per = key_len ? std::max<uint64_t>(1, stage_bytes() / key_len) : (uint64_t)1 << 22;
   const uint64_t chunk = std::min<uint64_t>(per, n);
@@ -372,31 +496,43 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     }
     const uint64_t cnt = i1 - i0;
     const size_t nb = (size_t)(offsets[i1] - base);
+    const bool big = nb > stage;  // one key larger than the stage: a temporary buffer, not bigger slots
+    const size_t in_need = big ? 1 : std::max(nb, (size_t)1);
     const size_t need_keys = (size_t)std::max<uint64_t>(cnt, max_keys);
-    if (nb > c->in_cap || need_keys > c->key_cap || c->n_staged < ns) {
+    if (in_need > c->in_cap || need_keys > c->key_cap || c->n_staged < ns) {
       // growing the staging buffers frees them: collect every chunk in flight first
       for (int s = 0; s < ns; ++s)
         if ((rc = drain_slot(c, s, pend[s]))) return rc;
-      if ((rc = ensure_staging(c, std::max(nb, (size_t)1), need_keys, ns))) return rc;
+      if ((rc = ensure_staging(c, in_need, need_keys, ns))) return rc;
     }
     if (job.probe && (rc = ensure_probe_staging(c))) return rc;
     const int s = (int)(idx % ns);
-    if ((rc = drain_slot(c, s, pend[s]))) return rc;
-    if (nb && !in_pinned) par_memcpy(c->h_in[s], bytes + base, nb);
+    TmpDevBuf tmp;
+    if (big) {
+      for (int q = 0; q < ns; ++q)
+        if ((rc = drain_slot(c, q, pend[q]))) return rc;
+      HB_TRY(hipMalloc(&tmp.p, nb));
+    } else if ((rc = drain_slot(c, s, pend[s]))) {
+      return rc;
+    }
+    uint8_t* d_in = big ? (uint8_t*)tmp.p : c->d_in[s];
+    if (nb && !in_pinned && !big) par_memcpy(c->h_in[s], bytes + base, nb);
     const uint64_t* off_src = offsets + i0;
     if (!off_pinned) {
       par_memcpy(c->h_off[s], offsets + i0, (cnt + 1) * sizeof(uint64_t));
       off_src = c->h_off[s];
     }
-    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], in_pinned ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
-                                  c->st[s]));
+    if (nb)
+      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || big) ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
+                            c->st[s]));
     HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
     shfhb::Sink k;
     int mode = 0;
     job_sink(c, s, job, &k, &mode);
     // the chunk's byte count sizes the span kernel's window (kernels.hip span_window)
-    HB_TRY(shfhb::launch_var(c->d_in[s], c->d_off[s], base, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto, nb));
+    HB_TRY(shfhb::launch_var(d_in, c->d_off[s], base, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto, nb));
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
+    if (big && (rc = drain_slot(c, s, pend[s]))) return rc;  // before tmp is freed
     i0 = i1;
   }
   for (int s = 0; s < ns; ++s)
@@ -450,14 +586,30 @@ int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, 
   return SHF_HB_OK;
 }
 
+// Device-resident variable-length keys. The offsets are only on the device, so
+// the kernels check them (o1 < o0 or o1 - o0 >= 2^31: kernels.hip var_key_bad),
+// skip such keys without reading their bytes and set a status word:
+// synchronous calls clear and read their own word and return SHF_HB_ERR_ARG;
+// asynchronous ones set the thread's sticky word, read by shf_hash_batch_status().
 int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const shfhb::Sink& sink,
                int out_mode, hipStream_t st, bool sync, int kernel = shfhb::kKernelAuto, uint64_t key_bytes = 0) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  if (sync) st = c->st[0];
-  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, sink, out_mode, st, kernel, key_bytes));
-  if (sync) HB_TRY(hipStreamSynchronize(st));
+  shfhb::Sink k = sink;
+  if (sync) {
+    st = c->st[0];
+    k.status = c->d_status + 1;
+    HB_TRY(hipMemsetAsync(k.status, 0, sizeof(uint32_t), st));
+  } else {
+    k.status = c->d_status;
+  }
+  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, k, out_mode, st, kernel, key_bytes));
+  if (sync) {
+    HB_TRY(hipMemcpyAsync(c->h_status, k.status, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HB_TRY(hipStreamSynchronize(st));
+    if (*c->h_status) return SHF_HB_ERR_ARG;
+  }
   return SHF_HB_OK;
 }
 
@@ -503,12 +655,21 @@ int visible_devices() {
   return n;
 }
 
+// Test-only knob SHF_HB_MULTI_SHARE_DEVICES=1: shard d runs on device
+// d % visible, so n_devices may exceed the visible devices (exercises the
+// multi-GPU split with several host threads on a one-GPU box).
+bool multi_share_devices() {
+  const char* e = getenv("SHF_HB_MULTI_SHARE_DEVICES");
+  return e && e[0] == '1';
+}
+
 template <class F>
 int run_multi(uint64_t n, int n_devices, F&& shard_fn) {
   const int vis = visible_devices();
   if (vis < 0) return vis;
   if (vis == 0) return SHF_HB_ERR_NODEV;
-  int g = n_devices <= 0 ? vis : std::min(n_devices, vis);
+  const bool share = multi_share_devices();
+  int g = n_devices <= 0 ? vis : (share ? std::min(n_devices, 64) : std::min(n_devices, vis));
   if ((uint64_t)g > n) g = (int)std::max<uint64_t>(1, n);
   std::vector<int> rcs(g, SHF_HB_OK);
   std::vector<int> errs(g, 0);
@@ -516,7 +677,7 @@ int run_multi(uint64_t n, int n_devices, F&& shard_fn) {
   for (int d = 0; d < g; ++d) {
     const uint64_t lo = n * (uint64_t)d / (uint64_t)g, hi = n * (uint64_t)(d + 1) / (uint64_t)g;
     th.emplace_back([&, d, lo, hi]() {
-      hipError_t e = hipSetDevice(d);
+      hipError_t e = hipSetDevice(d % vis);
       if (e != hipSuccess) {
         rcs[d] = map_hip(e);
       } else if (hi > lo) {
@@ -783,6 +944,18 @@ int shf_probe_batch_hashes_async(const shf_row_index* index, const shf_hash128* 
   if ((rc = current_ctx(&c))) return rc;
   HB_TRY(shfhb::launch_probe_hashes(d_hashes, n, sink, (hipStream_t)hip_stream));
   return SHF_HB_OK;
+}
+
+int shf_hash_batch_status(void* hip_stream) {
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  HB_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
+  uint32_t v = 0;
+  HB_TRY(hipMemcpy(&v, c->d_status, sizeof(v), hipMemcpyDeviceToHost));
+  if (!v) return SHF_HB_OK;
+  HB_TRY(hipMemset(c->d_status, 0, sizeof(v)));
+  return SHF_HB_ERR_ARG;
 }
 
 int shf_hash_batch_device_count(void) { return visible_devices(); }

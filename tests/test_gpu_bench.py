@@ -1,0 +1,59 @@
+"""bench.py's multi-rank path on the GPU box (configs[4]'s split):
+
+* `bench.py --gpus 2` with one visible GPU is refused (every rank needs a GPU
+  of its own);
+* the same run as a labelled rehearsal (--allow-shared-gpu) spawns 2 rank
+  processes that each hash their own contiguous shard of the 1B keys through
+  the product library: shards [0, 5e8) and [5e8, 1e9), disjoint and complete,
+  outputs checked against the oracle on every rank, `n_gpus` = distinct GPUs.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--only", "fixed16,shard1b", "--steps", "5", "--warmup", "2", "--repeats", "2", "--rotate", "2",
+        "--keys16", "1000000", "--no-cpu", "--traffic", "off", "--no-host-inclusive", "--warmup-min-s", "0",
+        "--quiet"]
+
+
+def _env():
+    return {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+
+
+def _run(extra, timeout=240):
+    return subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2"] + ARGS + extra,
+                          capture_output=True, text=True, timeout=timeout, env=_env(), cwd=ROOT)
+
+
+def test_two_ranks_refused_on_one_gpu():
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two GPUs visible: nothing to refuse")
+    p = _run([])
+    assert p.returncode != 0
+    assert "GPU(s) visible" in p.stderr
+    assert p.stdout.strip() == ""
+
+
+def test_two_rank_rehearsal_shards_configs4():
+    p = _run(["--allow-shared-gpu"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    ndev = torch.cuda.device_count()
+    assert line["ranks"] == 2
+    assert line["n_gpus"] == min(2, ndev)
+    assert line.get("rehearsal", False) == (ndev < 2)
+    sh = line["secondary"]["shard1b"]
+    assert sh["scaling"] == "strong"
+    assert sh["shards"] == [[0, 500_000_000], [500_000_000, 1_000_000_000]]
+    assert sh["verified"]["ok"] is True and sh["verified"]["samples_per_rank"] >= 20000
+    assert line["verified"] is True
+    # value = all ranks' keys / max-over-ranks time
+    assert line["value"] == pytest.approx(2 * 1_000_000 * 5 / (line["ms_per_step"] * 5 / 1e3), rel=1e-6)

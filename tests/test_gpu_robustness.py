@@ -1,0 +1,212 @@
+"""Robustness of the product path on the GPU (through the C ABI):
+
+* malformed device-resident offsets (include/shf_hash_batch.h Conventions): the
+  kernels skip invalid keys without reading their bytes, still hash every valid
+  key bit-exact, and the call reports SHF_HB_ERR_ARG (sync) or through
+  shf_hash_batch_status() (async) -- never a GPU fault;
+* the Python binding's argument checks (dtype, device, shape) before any launch;
+* per-thread resources: short-lived caller threads leave no streams, pinned or
+  device staging behind (the reference's usage model is many processes and
+  threads on one box, /root/reference/README.md:25-27);
+* the multi-device split (run_multi) with several host threads sharing one GPU
+  (test-only knob SHF_HB_MULTI_SHARE_DEVICES).
+"""
+import ctypes
+import gc
+import threading
+
+import numpy as np
+import pytest
+
+from sharedhashfile_amd.keygen import splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+SENTINEL = np.uint64(0xDEADBEEFDEADBEEF)
+VAR_KERNELS = [0, 3, 4, 5]  # AUTO, GENERIC, SPAN, ROUND
+
+
+@pytest.fixture(scope="module")
+def dev(hb):
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    hb.check_device()
+    return torch.device("cuda:0")
+
+
+def _malformed(n=1000, seed=3):
+    """A batch with invalid keys: 99 (offsets decrease), 499 (length 2^31), 500
+    (it starts at 499's end: decreasing), 777 (length 2^31 + 5) and 778."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 300, size=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(splitmix_bytes(int(off[-1]) + 64, seed), dtype=np.uint8).copy()
+    off[100] = off[99] - np.uint64(5)
+    off[500] = off[499] + np.uint64(1 << 31)
+    off[778] = off[777] + np.uint64((1 << 31) + 5)
+    bad = {99, 499, 500, 777, 778}
+    return data, off, bad
+
+
+def _want(oracle, data, off, bad):
+    n = off.size - 1
+    want = np.empty((n, 2), dtype=np.uint64)
+    for i in range(n):
+        if i in bad:
+            want[i] = SENTINEL
+        else:
+            o0, o1 = int(off[i]), int(off[i + 1])
+            want[i] = oracle.hash_var(data[o0:o1], np.array([0, o1 - o0], dtype=np.uint64))[0]
+    return want
+
+
+def _dev_bufs(data, off, n, dev):
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(off.view(np.int64)).to(dev)
+    out = torch.full((n, 2), int(SENTINEL.view(np.int64)), dtype=torch.int64, device=dev)
+    return d, o, out
+
+
+@pytest.mark.parametrize("kernel", VAR_KERNELS)
+def test_malformed_offsets_async_status(hb, dev, oracle, kernel):
+    lib = hb.load()
+    data, off, bad = _malformed()
+    n = off.size - 1
+    want = _want(oracle, data, off, bad)
+    d, o, out = _dev_bufs(data, off, n, dev)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.shf_hash_batch_status(s) == hb.OK  # nothing pending
+    assert lib.shf_hash_batch_var_kernel_async(d.data_ptr(), o.data_ptr(), n, 12345, out.data_ptr(), kernel, s) == 0
+    assert lib.shf_hash_batch_status(s) == hb.ERR_ARG
+    assert lib.shf_hash_batch_status(s) == hb.OK  # the query cleared it
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want)
+    # sized entry point (span window from the byte count), Python binding + status()
+    out.fill_(int(SENTINEL.view(np.int64)))
+    hb.hash_var(d, o, out=out, kernel=kernel, key_bytes=int(off[-1]))
+    with pytest.raises(hb.ShfHashBatchError) as ei:
+        hb.status()
+    assert ei.value.status == hb.ERR_ARG
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want)
+
+
+def test_malformed_offsets_sync_and_other_outputs(hb, dev, oracle):
+    lib = hb.load()
+    data, off, bad = _malformed(seed=4)
+    n = off.size - 1
+    want = _want(oracle, data, off, bad)
+    d, o, out = _dev_bufs(data, off, n, dev)
+    assert lib.shf_hash_batch_var(d.data_ptr(), o.data_ptr(), n, 12345, out.data_ptr(), hb.MEM_DEVICE) == hb.ERR_ARG
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want)
+    # a valid batch through the same sync entry point is OK again (its own status word)
+    good = np.arange(0, 1001, dtype=np.uint64) * np.uint64(7)
+    og = torch.from_numpy(good.view(np.int64)).to(dev)
+    assert lib.shf_hash_batch_var(d.data_ptr(), og.data_ptr(), 1000, 12345, out.data_ptr(), hb.MEM_DEVICE) == hb.OK
+    # UID parts and probe (async) report through the status word
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    parts = torch.zeros(n, dtype=torch.int64, device=dev)
+    assert lib.shf_uid_parts_batch_var_async(d.data_ptr(), o.data_ptr(), n, 12345, parts.data_ptr(), s) == 0
+    assert lib.shf_hash_batch_status(s) == hb.ERR_ARG
+    ok = np.array([i for i in range(n) if i not in bad])
+    assert np.array_equal(parts.cpu().numpy().view(np.uint64)[ok], oracle.uid_parts(want[ok]))
+    idx = hb.RowIndex(4)
+    rec = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+    assert lib.shf_probe_batch_var_async(idx.handle, d.data_ptr(), o.data_ptr(), n, 12345, None, rec.data_ptr(),
+                                         s) == 0
+    assert lib.shf_hash_batch_status(s) == hb.ERR_ARG
+    assert lib.shf_probe_batch_var(idx.handle, d.data_ptr(), o.data_ptr(), n, 12345, None, rec.data_ptr(),
+                                   hb.MEM_DEVICE) == hb.ERR_ARG
+    idx.close()
+    torch.cuda.synchronize()
+
+
+def test_python_binding_rejects_bad_arguments(hb, dev):
+    keys = torch.zeros(64, dtype=torch.uint8, device=dev)
+    with pytest.raises(TypeError):
+        hb.hash_fixed(keys.view(torch.int64), 16)  # not uint8: would count elements, not bytes
+    with pytest.raises(TypeError):
+        hb.hash_fixed(torch.zeros(64, dtype=torch.uint8), 16)  # host tensor
+    with pytest.raises(ValueError):
+        hb.hash_fixed(keys.view(8, 8).t(), 16)  # not contiguous
+    with pytest.raises(ValueError):
+        hb.hash_fixed(keys, 16, out=torch.zeros((3, 2), dtype=torch.int64, device=dev))  # wrong shape
+    off = torch.tensor([0, 8, 16], dtype=torch.int64, device=dev)
+    with pytest.raises(TypeError):
+        hb.hash_var(keys, off.to(torch.int32))
+    with pytest.raises(TypeError):
+        hb.hash_var(keys, off.cpu())
+    with pytest.raises(ValueError):
+        hb.hash_var(keys, off, out=torch.zeros((3, 2), dtype=torch.int64, device=dev))
+    with pytest.raises(ValueError):
+        hb.hash_var(keys, off.view(3, 1))
+
+
+def test_short_lived_threads_release_their_contexts(hb, dev, oracle):
+    """64 threads each hash a host batch (32 MiB of keys: full-size staging of
+    3 slots = ~240 MiB pinned + ~240 MiB device per thread) and exit; their
+    streams and staging must go with them."""
+    import psutil
+
+    lib = hb.load()
+    n = 2 << 20
+    keys = np.frombuffer(splitmix_bytes(n * 16, 41), dtype=np.uint8)
+    idx = np.unique(np.random.default_rng(1).integers(0, n, size=20000))
+    want = oracle.hash_fixed(keys.reshape(n, 16)[idx], 16)
+    results = []
+
+    def call():
+        out = np.empty((n, 2), dtype=np.uint64)
+        rc = lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, 12345, out.ctypes.data, hb.MEM_HOST)
+        results.append(rc == 0 and np.array_equal(out[idx], want))
+
+    def wave(k):
+        ts = [threading.Thread(target=call) for _ in range(k)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+
+    wave(1)  # runtime and copy-pool warm-up
+    gc.collect()
+    proc = psutil.Process()
+    rss0, free0 = proc.memory_info().rss, torch.cuda.mem_get_info()[0]
+    for _ in range(8):
+        wave(8)
+    gc.collect()
+    rss1, free1 = proc.memory_info().rss, torch.cuda.mem_get_info()[0]
+    assert len(results) == 65 and all(results)
+    leaked_host, leaked_dev = rss1 - rss0, free0 - free1
+    # a leak would be ~64 x 240 MiB on each side
+    assert leaked_dev < (512 << 20), leaked_dev
+    assert leaked_host < (2 << 30), leaked_host
+
+
+@pytest.mark.parametrize("n_devices", [2, 3])
+def test_multi_split_with_shared_device(hb, dev, oracle, monkeypatch, n_devices):
+    """shf_hash_batch_*_multi's split (one host thread per shard, contiguous key
+    ranges, results into disjoint slices) with the shards sharing this GPU."""
+    monkeypatch.setenv("SHF_HB_MULTI_SHARE_DEVICES", "1")
+    n = 1_000_003
+    flat = np.frombuffer(splitmix_bytes(n * 16, 51), dtype=np.uint8)
+    assert np.array_equal(hb.hash_fixed_host(flat, 16, n_devices=n_devices), oracle.hash_fixed(flat, 16, threads=8))
+    rng = np.random.default_rng(n_devices)
+    m = 200_001
+    lens = rng.integers(0, 600, size=m)
+    off = np.zeros(m + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    assert np.array_equal(hb.hash_var_host(data, off, n_devices=n_devices), oracle.hash_var(data, off))
+    # fewer keys than shards: the split shrinks, nothing is dropped
+    assert np.array_equal(hb.hash_fixed_host(flat[:32], 16, n_devices=n_devices), oracle.hash_fixed(flat[:32], 16))
+
+
+def test_host_keys_larger_than_the_stage(hb, dev, oracle, monkeypatch):
+    """A fixed key and a variable key larger than SHF_HB_STAGE_MB go through a
+    temporary device buffer (the slots keep their stage size)."""
+    monkeypatch.setenv("SHF_HB_STAGE_MB", "1")
+    big = (1 << 20) + 4099
+    flat = np.frombuffer(splitmix_bytes(3 * big, 61), dtype=np.uint8)
+    assert np.array_equal(hb.hash_fixed_host(flat, big), oracle.hash_fixed(flat, big))
+    off = np.array([0, 10, 10 + 3 * big - 100, 3 * big - 50, 3 * big], dtype=np.uint64)
+    assert np.array_equal(hb.hash_var_host(flat, off), oracle.hash_var(flat, off))

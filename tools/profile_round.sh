@@ -6,6 +6,6 @@ set -u
 out=$1; mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- \
-  python3 bench.py --steps 20 --warmup 3 --warmup-min-s 0 --no-cpu --traffic off > "$out/kt_bench.json" 2> "$out/kt_bench.err" || exit 1
-tools/pmc_run.sh "$out/pmc" --steps 3 --warmup 1 --warmup-min-s 0 --no-cpu --traffic off > "$out/pmc.log" 2>&1 || exit 2
+  python3 bench.py --steps 20 --warmup 3 --repeats 1 --warmup-min-s 0 --no-cpu --no-verify --no-host-inclusive --traffic off > "$out/kt_bench.json" 2> "$out/kt_bench.err" || exit 1
+tools/pmc_run.sh "$out/pmc" --steps 3 --warmup 1 --repeats 1 --warmup-min-s 0 --no-cpu --no-verify --no-host-inclusive --traffic off > "$out/pmc.log" 2>&1 || exit 2
 echo profile ok
