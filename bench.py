@@ -239,7 +239,7 @@ def verify_var(data, off, out, samples, seed):
     starts = torch.repeat_interleave(o0, lens)
     first = torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
     pos = starts + (torch.arange(starts.numel(), device=data.device) - first)
-    sub = data.index_select(0, pos).cpu().numpy()
+    sub = data[pos].cpu().numpy()
     hoff = np.zeros(idx.size + 1, dtype=np.uint64)
     hoff[1:] = np.cumsum(lens.cpu().numpy())
     got = out.index_select(0, ti).cpu().numpy().view(np.uint64)
@@ -312,11 +312,11 @@ def make_workloads(args, dev, rank, world=1):
         del lens
         vk = {"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]
         wl.append(Workload("var", n, total / n + 8 + 16,
-                           [lambda d=data, o=off, out=out: hb.hash_var(d, o, out=out, kernel=vk, key_bytes=total)],
+                           [lambda d=data, o=off, out=out, vk=vk, tb=total: hb.hash_var(d, o, out=out, kernel=vk, key_bytes=tb)],
                            {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel,
                                                                                                "k_span"),
                            "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9),
-                           lambda: verify_var(data, off, out, VERIFY_SAMPLES, 15)))
+                           lambda d=data, o=off, out=out: verify_var(d, o, out, VERIFY_SAMPLES, 15)))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding
         # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +

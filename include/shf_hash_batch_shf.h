@@ -1,0 +1,115 @@
+/*
+ * shf_hash_batch_shf.h -- the GPU batch hashes (shf_hash_batch.h) fed into
+ * SharedHashFile's unchanged put/get/del flow.
+ *
+ * The reference hashes one key per call, shf_make_hash(key, key_len)
+ * (/root/reference/src/shf.c:450-462), leaving the result in thread-locals that
+ * put/get/del read (SHF_HASH shf_hash, shf_hash_key, shf_hash_key_len:
+ * /root/reference/src/shf.private.h:187-189). Its tests already set those by
+ * hand for caller-supplied hashes (/root/reference/src/test.9.shf.c:176-182);
+ * this header packages that seam:
+ *
+ *   shf_use_hash()           the three assignments, from one shf_hash128 record
+ *   shf_put_batch_var()      INTEGRATION.md §3: hash a host batch on the GPU,
+ *                            then shf_put_key_val() per key
+ *   shf_get_batch_probed()   INTEGRATION.md §6: a get batch driven by row
+ *                            pre-probe records, falling back to the ordinary
+ *                            get with the batch hash
+ *
+ * Include it after the reference's shf.private.h and shf.h, in that order
+ * (shf.h names the types shf.private.h defines). Everything is static inline:
+ * SharedHashFile.a gains no symbol, the application links libshf_hash_batch.so
+ * and nothing else.
+ */
+#ifndef SHF_HASH_BATCH_SHF_H
+#define SHF_HASH_BATCH_SHF_H
+
+#ifndef __SHF_PRIVATE_H__
+#error "include the reference's shf.private.h and shf.h before shf_hash_batch_shf.h"
+#endif
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "shf_hash_batch.h"
+
+/* shf_make_hash(key, key_len) with the hash already computed (h = that key's
+ * record from a shf_hash_batch_* call). The key pointer is kept, not copied,
+ * exactly as shf_make_hash() keeps it (shf.c:460-461): it must stay valid
+ * until the put/get/del that follows. */
+static inline void shf_use_hash(const char *key, uint32_t key_len, const shf_hash128 *h)
+{
+    shf_hash.u64[0] = h->h1;
+    shf_hash.u64[1] = h->h2;
+    shf_hash_key = key;
+    shf_hash_key_len = key_len;
+}
+
+/* Put n host keys (key i = bytes[offsets[i] .. offsets[i+1])) with values
+ * (value i = vals[val_offsets[i] .. val_offsets[i+1])): one GPU batch hash
+ * (shf_hash_batch_var, SHF_HASH_MEM_HOST, seed 12345), then the reference's
+ * shf_put_key_val() per key. Returns the number of keys put (n, or the index
+ * of the first put that did not return SHF_RET_KEY_PUT), or a negative
+ * SHF_HB_ERR_* status with nothing put. */
+static inline int64_t shf_put_batch_var(SHF *shf, const char *bytes, const uint64_t *offsets, uint64_t n,
+                                        const char *vals, const uint64_t *val_offsets)
+{
+    if (n == 0) return 0;
+    shf_hash128 *h = (shf_hash128 *)malloc(n * sizeof *h);
+    if (!h) return SHF_HB_ERR_NOMEM;
+    const int rc = shf_hash_batch_var(bytes, offsets, n, SHF_HASH_BATCH_SEED, h, SHF_HASH_MEM_HOST);
+    if (rc != SHF_HB_OK) {
+        free(h);
+        return rc;
+    }
+    uint64_t i = 0;
+    for (; i < n; ++i) {
+        shf_use_hash(bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]), &h[i]);
+        if (shf_put_key_val(shf, vals + val_offsets[i], (uint32_t)(val_offsets[i + 1] - val_offsets[i])) !=
+            SHF_RET_KEY_PUT)
+            break;
+    }
+    free(h);
+    return (int64_t)i;
+}
+
+/* Get n host keys, given their hashes and row pre-probe records (from
+ * shf_probe_batch_var / _fixed against a row index of this store):
+ *   a candidate ref  -> shf_get_uid_val_copy(uid) (shf.c:1037, which checks
+ *                       the ref's pos and tab but not the key), then the
+ *                       stored key is compared with key i;
+ *   otherwise        -> shf_get_key_val_copy() with the batch hash in the
+ *                       seam: found or not, exactly as the reference decides.
+ * The index is a snapshot, so a stale candidate only costs the fast path.
+ * For every key found, shf_val / shf_val_len hold its value when on_found(ctx, i)
+ * is called. Returns the keys found; *fast (if not NULL) = those served by the
+ * uid path. */
+static inline uint64_t shf_get_batch_probed(SHF *shf, const char *bytes, const uint64_t *offsets, uint64_t n,
+                                            const shf_hash128 *hashes, const shf_probe *probes,
+                                            void (*on_found)(void *ctx, uint64_t i), void *ctx, uint64_t *fast)
+{
+    uint64_t found = 0, f = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const char *k = bytes + offsets[i];
+        const uint32_t kl = (uint32_t)(offsets[i + 1] - offsets[i]);
+        if (probes[i].mask && shf_get_uid_val_copy(shf, probes[i].uid) == SHF_RET_KEY_FOUND) {
+            uint32_t stored_len = shf->fixed_key_len; /* fixed-length stores keep no length (shf.c:927) */
+            if (!shf->is_fixed_key_val_len) memcpy(&stored_len, (const char *)shf_key_addr - 4, 4);
+            if (stored_len == kl && memcmp(shf_key_addr, k, kl) == 0) {
+                ++found;
+                ++f;
+                if (on_found) on_found(ctx, i);
+                continue;
+            }
+        }
+        shf_use_hash(k, kl, &hashes[i]);
+        if (shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND) {
+            ++found;
+            if (on_found) on_found(ctx, i);
+        }
+    }
+    if (fast) *fast = f;
+    return found;
+}
+
+#endif /* SHF_HASH_BATCH_SHF_H */

@@ -59,10 +59,20 @@ def build_oracle(verbose=True):
     subprocess.check_call(cmd)
 
 
+def build_c_tests(verbose=True):
+    """tests/c/build/test_seam (the seam proven from C), where the reference's
+    headers exist to compile it; elsewhere the prebuilt binary is used."""
+    cmd = ["make", "-s", "-C", os.path.join(ROOT, "tests", "c")]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     build_library(force="--force" in argv)
     build_oracle()
+    build_c_tests()
 
 
 if __name__ == "__main__":

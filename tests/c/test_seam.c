@@ -1,0 +1,179 @@
+/*
+ * The drop-in seam, proven from C (no ctypes): this program links
+ * libshf_hash_batch.so (the product) with the reference's own table engine
+ * (src/shf.c + src/murmurhash3.c, compiled by oracle/Makefile into oracle/_ref/)
+ * and runs, on one store:
+ *
+ *   1. INTEGRATION.md §3's batched put loop: shf_put_batch_var() -- one GPU
+ *      batch hash (shf_hash_batch_var, host memory), then shf_use_hash() +
+ *      shf_put_key_val() per key (include/shf_hash_batch_shf.h);
+ *   2. the reference's own get loop (shf_make_hash() + shf_get_key_val_copy(),
+ *      test.9.shf.c:442-445 shape) over the stored keys and as many absent
+ *      ones: every stored key found with its value, no absent key found;
+ *   3. INTEGRATION.md §6's probed get loop: the store's rows exported into a
+ *      row index, the whole batch hashed and probed on the GPU
+ *      (shf_probe_batch_var, host memory), shf_get_batch_probed(): the same
+ *      answers, most stored keys served by the uid path;
+ *   4. fixed 16-byte keys: shf_hash_batch_fixed + shf_use_hash + put, then
+ *      the reference's get with its CPU hash finds every one.
+ *
+ * TEST INFRASTRUCTURE: built by tests/c/Makefile where /root/reference exists
+ * (the reference's headers are needed to compile it), into tests/c/build/, which
+ * travels to the GPU box with the tree. Exit status: 0 pass, 1 fail, 2 no usable
+ * GPU (the library refused: no CPU fallback).
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "shf.private.h"
+#include "shf.h"
+#include "shf_hash_batch_shf.h"
+
+/* oracle/ref_export.c (test infrastructure): rows + tab map of a store */
+extern int64_t ref_export_rows(SHF *shf, uint32_t *tab_slot, uint8_t *rows, uint64_t max_slots);
+
+static uint64_t splitmix(uint64_t *s)
+{
+    uint64_t z = (*s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+static int fail(const char *what)
+{
+    fprintf(stderr, "test_seam: FAIL: %s\n", what);
+    return 1;
+}
+
+static uint64_t good_values;
+static void check_value(void *ctx, uint64_t i)
+{
+    (void)ctx;
+    good_values += shf_val_len == sizeof(i) && memcmp(shf_val, &i, sizeof(i)) == 0;
+}
+
+int main(int argc, char **argv)
+{
+    const uint64_t n_put = argc > 1 ? strtoull(argv[1], 0, 10) : 200000, n_absent = n_put / 10;
+    const uint64_t n = n_put + n_absent;
+    const int rc0 = shf_hash_batch_check_device();
+    if (rc0 != SHF_HB_OK) {
+        fprintf(stderr, "test_seam: no usable GPU: %s\n", shf_hash_batch_strerror(rc0));
+        return 2;
+    }
+
+    /* keys 4..67 bytes, unique (the key index in their first 4-8 bytes), values = the key index (8 bytes) */
+    uint64_t *off = malloc((n + 1) * sizeof *off), *voff = malloc((n + 1) * sizeof *voff);
+    uint64_t st = 0x5348460000000077ull;
+    off[0] = voff[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        off[i + 1] = off[i] + 4 + splitmix(&st) % 64;
+        voff[i + 1] = voff[i] + 8;
+    }
+    char *bytes = malloc(off[n] + 8), *vals = malloc(8 * n);
+    for (uint64_t b = 0; b < off[n]; b += 8) {
+        const uint64_t v = splitmix(&st);
+        memcpy(bytes + b, &v, 8);
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t len = off[i + 1] - off[i];
+        memcpy(bytes + off[i], &i, len < 8 ? len : 8);
+        memcpy(vals + 8 * i, &i, 8);
+    }
+    char folder[] = "/dev/shm/seamXXXXXX";
+    if (!mkdtemp(folder)) return fail("mkdtemp");
+    shf_init();
+    SHF *shf = shf_attach(folder, "seam", 0);
+    if (!shf) return fail("shf_attach");
+
+    /* 1. batched put with GPU hashes */
+    const int64_t put = shf_put_batch_var(shf, bytes, off, n_put, vals, voff);
+    if (put != (int64_t)n_put) {
+        fprintf(stderr, "put %lld of %llu\n", (long long)put, (unsigned long long)n_put);
+        return fail("shf_put_batch_var");
+    }
+
+    /* 2. the reference's own get (CPU hash): the answer of record, per key */
+    uint8_t *want_found = calloc(n, 1);
+    uint64_t *want_val = calloc(n, sizeof *want_val);
+    uint64_t ref_found = 0, ref_right = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        shf_make_hash(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        if (shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND) {
+            want_found[i] = 1;
+            memcpy(&want_val[i], shf_val, 8);
+            ++ref_found;
+            ref_right += i < n_put && want_val[i] == i;
+        }
+    }
+    /* every stored key found with its own value, no absent key found */
+    if (ref_right != n_put || ref_found != n_put) return fail("reference get after GPU-hashed put");
+
+    /* 3. probed get: export, index, probe on the GPU, the §6 loop */
+    const uint64_t max_slots = 4096;
+    uint32_t *tab_slot = malloc(SHF_ROW_INDEX_TABS * sizeof *tab_slot);
+    uint8_t *rows = malloc(max_slots * SHF_ROW_INDEX_SLOT_BYTES);
+    const int64_t slots = ref_export_rows(shf, tab_slot, rows, max_slots);
+    if (slots <= 0) return fail("ref_export_rows");
+    shf_row_index *ix = NULL;
+    if (shf_row_index_create((uint64_t)slots, &ix) != SHF_HB_OK) return fail("shf_row_index_create");
+    if (shf_row_index_set_tabs(ix, tab_slot) != SHF_HB_OK) return fail("set_tabs");
+    if (shf_row_index_set_rows(ix, 0, (uint64_t)slots, rows) != SHF_HB_OK) return fail("set_rows");
+    shf_hash128 *h = malloc(n * sizeof *h);
+    shf_probe *pr = malloc(n * sizeof *pr);
+    if (shf_probe_batch_var(ix, bytes, off, n, SHF_HASH_BATCH_SEED, h, pr, SHF_HASH_MEM_HOST) != SHF_HB_OK)
+        return fail("shf_probe_batch_var");
+    uint64_t fast = 0;
+    good_values = 0;
+    const uint64_t found = shf_get_batch_probed(shf, bytes, off, n, h, pr, check_value, NULL, &fast);
+    /* the probed loop must give the reference's answers: same found count, every stored key's value */
+    if (found != ref_found) return fail("probed get: found count differs from the reference's get");
+    if (good_values != ref_right) return fail("probed get: values differ from the reference's get");
+    if (fast < n_put / 2) return fail("probed get: uid path unused");
+    /* GPU hash == CPU shf_make_hash for every key */
+    for (uint64_t i = 0; i < n; ++i) {
+        shf_make_hash(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        if (shf_hash.u64[0] != h[i].h1 || shf_hash.u64[1] != h[i].h2) return fail("GPU hash != shf_make_hash");
+    }
+    shf_row_index_destroy(ix);
+
+    /* 4. fixed 16-byte keys */
+    const uint64_t nf = 50000;
+    char *fk = malloc(16 * nf);
+    for (uint64_t i = 0; i < 2 * nf; ++i) {
+        const uint64_t v = splitmix(&st);
+        memcpy(fk + 8 * i, &v, 8);
+    }
+    for (uint64_t i = 0; i < nf; ++i) memcpy(fk + 16 * i, &i, 8);
+    shf_hash128 *fh = malloc(nf * sizeof *fh);
+    if (shf_hash_batch_fixed(fk, 16, nf, SHF_HASH_BATCH_SEED, fh, SHF_HASH_MEM_HOST) != SHF_HB_OK)
+        return fail("shf_hash_batch_fixed");
+    char fshf_name[] = "seamfixed";
+    SHF *fshf = shf_attach(folder, fshf_name, 0);
+    if (!fshf) return fail("shf_attach fixed");
+    for (uint64_t i = 0; i < nf; ++i) {
+        shf_use_hash(fk + 16 * i, 16, &fh[i]);
+        if (shf_put_key_val(fshf, (const char *)&i, 8) != SHF_RET_KEY_PUT) return fail("fixed put");
+    }
+    uint64_t ffound = 0;
+    for (uint64_t i = 0; i < nf; ++i) {
+        shf_make_hash(fk + 16 * i, 16);
+        ffound += shf_get_key_val_copy(fshf) == SHF_RET_KEY_FOUND && memcmp(shf_val, &i, 8) == 0;
+    }
+    if (ffound != nf) return fail("fixed keys: reference get after GPU-hashed put");
+
+    printf("{\"n_put\": %llu, \"n_query\": %llu, \"ref_found\": %llu, \"ref_right\": %llu, \"probed_found\": %llu, "
+           "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu}\n",
+           (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
+           (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
+           (unsigned long long)ffound);
+    (void)shf_del(shf);
+    (void)shf_del(fshf);
+    rmdir(folder);
+    return 0;
+}

@@ -1,0 +1,66 @@
+"""The drop-in seam from C: tests/c/test_seam.c links libshf_hash_batch.so with
+the reference's own table engine (oracle/_ref) and runs INTEGRATION.md §3's
+batched put loop and §6's probed get loop through include/shf_hash_batch_shf.h
+(no ctypes). Built by tests/c/Makefile where /root/reference exists; the binary
+travels to the GPU box in tests/c/build/.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "c", "build", "test_seam")
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def _need_bin():
+    if not os.path.exists(BIN):
+        pytest.skip("tests/c/build/test_seam not built (needs /root/reference headers at build time)")
+
+
+def test_seam_header_compiles_against_reference_headers():
+    if not os.path.isdir("/root/reference/src"):
+        pytest.skip("reference headers absent")
+    src = ('#include "shf.private.h"\n#include "shf.h"\n#include "shf_hash_batch_shf.h"\n'
+           'int main(void){ shf_hash128 h = {1, 2}; shf_use_hash("k", 1, &h);'
+           ' return shf_hash.u64[0] == 1 && shf_hash_key_len == 1 ? 0 : 1; }\n')
+    p = subprocess.run(["gcc", "-std=gnu99", "-Wall", "-Werror", "-Wno-address-of-packed-member", "-fsyntax-only",
+                        "-I", os.path.join(ROOT, "include"), "-I", "/root/reference/src", "-x", "c", "-"],
+                       input=src.encode(), capture_output=True)
+    assert p.returncode == 0, p.stderr.decode()
+
+
+def test_seam_header_refuses_without_reference_private_header():
+    src = '#include "shf_hash_batch_shf.h"\nint main(void){return 0;}\n'
+    p = subprocess.run(["gcc", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), "-x", "c", "-"],
+                       input=src.encode(), capture_output=True)
+    assert p.returncode != 0 and b"shf.private.h" in p.stderr
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device behaviour")
+def test_seam_program_fails_loudly_without_gpu():
+    _need_bin()
+    p = subprocess.run([BIN, "1000"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2, (p.returncode, p.stderr)
+    assert "no usable GPU" in p.stderr
+
+
+@pytest.mark.gpu
+def test_seam_program_put_and_probed_get():
+    _need_bin()
+    p = subprocess.run([BIN, "200000"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["ref_found"] == r["n_put"] == r["ref_right"] == r["probed_found"] == 200000
+    assert r["probed_fast"] > 0.9 * r["n_put"]
+    assert r["fixed_found"] == 50000
