@@ -61,7 +61,7 @@ BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for 
 
 # rocprofv3 kernel-name substrings of each workload's kernel (PMC passes)
 KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
-               "fixed256": "k_tiled<0, 8>", "var": "k_span<0, true", "probe16": "k_fixed16<2>"}
+               "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>"}
 
 
 def parse(argv=None):
@@ -313,8 +313,8 @@ def make_workloads(args, dev, rank, world=1):
         vk = {"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]
         wl.append(Workload("var", n, total / n + 8 + 16,
                            [lambda d=data, o=off, out=out, vk=vk, tb=total: hb.hash_var(d, o, out=out, kernel=vk, key_bytes=tb)],
-                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel,
-                                                                                               "k_span"),
+                           {"generic": "k_generic", "round": "k_vround", "span": "k_span_pp"}.get(args.var_kernel,
+                                                                                                  "k_span_pp"),
                            "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9),
                            lambda d=data, o=off, out=out: verify_var(d, o, out, VERIFY_SAMPLES, 15)))
     if "probe16" in only:

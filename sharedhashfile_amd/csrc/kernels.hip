@@ -553,7 +553,7 @@ struct SpanTile {
   uint64_t key;       // this lane's key index
   uint64_t start;     // byte offset of this lane's key (relative to `bytes`)
   uint32_t len;       // this lane's key length
-  bool valid;         // key < n
+  uint32_t valid;     // key < n (not bool: keeps the struct out of scratch when copied)
   uint64_t base;      // absolute address of the span's first 16-B piece (uniform)
   uint32_t span16;    // bytes to stage, multiple of 16 (uniform; > kSpanCap -> fallback)
 };
@@ -698,6 +698,53 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
     const uint32_t d3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
     const uint64_t t1 = pack64(d0, d1) & low_bytes_mask(rem);
     const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
+    tail_block(s, t1, t2, rem);
+  }
+  finish(s, len);
+  return s;
+}
+
+#ifndef SHFHB_LDS_UNALIGNED
+#define SHFHB_LDS_UNALIGNED 1  // variable-length k_span: U[8,512] B keys +4-8 % (profiles/r2/ab_span/)
+#endif
+#ifndef SHFHB_SPAN_PINGPONG
+#define SHFHB_SPAN_PINGPONG 1  // k_span_pp for variable-length windows over 10 KiB
+#endif
+
+// hash_lds with one unaligned ds_read_b128 per block instead of dword reads
+// funnel-shifted by v_alignbyte_b32 (gfx950 runs LDS accesses in unaligned
+// mode; hipcc emits ds_read_b128 for an align-1 vector LDS load).
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(3))) const u32x4_a1 lds_u32x4_a1;
+
+__device__ __forceinline__ u32x4 lds_read16(const uint32_t* lds, uint32_t byte) {
+  return *(lds_u32x4_a1*)((lds_u8*)lds + byte);  // generic -> LDS address space (lds is an LDS pointer)
+}
+
+__device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
+  const uint32_t nblocks = len >> 4;
+  State s{seed, seed};
+  // software pipeline: block j's chain beside block j+1's mixes and block j+2's read
+  // (the compiler folds this loop-carried read into one read at the point of
+  // use; forcing it a block ahead -- an opaque copy plus a sched_barrier --
+  // measured no faster, profiles/r2/ab_span/)
+  u32x4 cur = lds_read16(lds, p);
+  u32x4 nxt = lds_read16(lds, p + 16u);
+  uint64_t m1 = mix_k1(pack64(cur.x, cur.y)), m2 = mix_k2(pack64(cur.z, cur.w));
+  for (uint32_t j = 0; j < nblocks; ++j) {
+    const u32x4 nn = lds_read16(lds, p + 16u * j + 32u);
+    const uint64_t n1 = mix_k1(pack64(nxt.x, nxt.y)), n2 = mix_k2(pack64(nxt.z, nxt.w));
+    chain_block(s, m1, m2);
+    m1 = n1;
+    m2 = n2;
+    cur = nxt;
+    nxt = nn;
+  }
+  const uint32_t rem = len & 15u;
+  if (rem) {  // cur holds the tail's bytes
+    const uint64_t t1 = pack64(cur.x, cur.y) & low_bytes_mask(rem);
+    const uint64_t t2 = rem > 8 ? (pack64(cur.z, cur.w) & low_bytes_mask(rem - 8)) : 0ull;
     tail_block(s, t1, t2, rem);
   }
   finish(s, len);
@@ -889,12 +936,74 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
     __syncthreads();
     if (ti.valid) {
       const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-      store_result<OUT>(sink, ti.key, hash_lds(span_lds, p, ti.len, seed));
+      // variable lengths: unaligned 16-B reads; fixed lengths keep the dword reads (L = 100, 200, 300 B:
+      // 4, 2, 9 % faster that way, profiles/r2/ab_span/)
+      store_result<OUT>(sink, ti.key, (SHFHB_LDS_UNALIGNED && VAR) ? hash_lds_u(span_lds, p, ti.len, seed)
+                                                                   : hash_lds(span_lds, p, ti.len, seed));
     }
   } else if constexpr (VAR && RFB) {  // span over the window: stream it in rounds (vround_tile) instead
     vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, reinterpret_cast<uint8_t*>(span_lds));
   } else if (ti.valid) {
     store_result<OUT>(sink, ti.key, hash_bytes(bytes + ti.start, ti.len, seed));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong span kernel (variable-length keys): two waves share one LDS
+// window and take turns. Both load their tile's span into registers at once;
+// wave 0 stages and hashes its tile while wave 1's span is still arriving,
+// then wave 1 stages and hashes. A window then holds bytes only while they are
+// staged or hashed (one HBM latency per two tiles instead of one per tile),
+// and a CU keeps twice as many hashing waves (4 per SIMD) for the same LDS.
+// U[8,512] B keys: +10 %, all-260 B: +15 %, U[200,400] B: +12 % over k_span
+// (profiles/r2/ab_span/). Tiles with an invalid key or a span over the window
+// are hashed per lane straight from HBM (few registers: the held span and the
+// hash must fit 128 VGPRs together).
+// (Two or more tiles per wave, each wave loading its next span right after
+// its hash, spill past 128 VGPRs; a persistent single-wave variant with the
+// next span prefetched into registers during the hash measured 0-10 % slower
+// than k_span: neither kept, git history.)
+// ---------------------------------------------------------------------------
+template <int OUT>
+__device__ __forceinline__ void span_tile_from_hbm(const uint8_t* bytes, uint64_t off_base, uint64_t n,
+                                                   const SpanRaw& raw, uint32_t lane, uint32_t seed, const Sink& sink) {
+  const uint64_t key = raw.t * 64u + lane;
+  if (var_key_bad(raw.o0, raw.o1)) flag_bad_key(sink);
+  else if (key < n)
+    store_result<OUT>(sink, key, hash_bytes(bytes + (raw.o0 - off_base), (uint32_t)(raw.o1 - raw.o0), seed));
+}
+
+template <int OUT, int PIECES>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_span_pp(
+    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
+    uint32_t seed, uint32_t cap, Sink sink) {
+  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
+  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t t = 2u * (uint64_t)blockIdx.x + wave;  // this wave's tile (past the last: idle, barriers only)
+  const uint64_t ntiles = (n + 63) / 64;
+  const bool has = t < ntiles;
+  const SpanRaw raw = span_load<true>(offsets, n, t, lane);  // keys past n: o0 = o1 = 0
+  const bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
+  const SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
+  const bool staged = has && !bad && ti.span16 <= cap;
+  u32x4 reg[PIECES];
+  if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
+#pragma unroll
+  for (uint32_t phase = 0; phase < 2; ++phase) {
+    if (wave == phase && staged) span_stage<PIECES>(span_lds, reg, ti.span16, lane);
+    __syncthreads();
+    if (wave == phase && has) {
+      if (staged) {
+        if (ti.valid) {
+          const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
+          store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, p, ti.len, seed));
+        }
+      } else {
+        span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -961,6 +1070,18 @@ static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint
 // at 10 vs 20 KiB, profiles/r1/ab_window/, ab_sized/).
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
+// Ping-pong span kernel: one 128-thread workgroup per two tiles, one window.
+template <int OUT>
+static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
+                                           uint32_t seed, const Sink& sink, hipStream_t st) {
+  const uint64_t tiles = (n + 63) / 64;
+  const uint64_t wgs = (tiles + 1) / 2;
+  if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_span_pp<OUT, kSpanPiecesMax>), dim3((unsigned)wgs), dim3(128), kSpanAlloc, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
+  return hipGetLastError();
+}
+
 template <int OUT, int PIECES, bool RFB>
 static hipError_t launch_var_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
                                   uint32_t seed, const Sink& sink, hipStream_t st, uint32_t need) {
@@ -986,6 +1107,10 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
                               uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0) {
   if constexpr (VAR) {
     const double need = key_bytes && n ? 64.0 * (double)key_bytes / (double)n * 1.1 + 512.0 + kSpanPad : 1e30;
+    // windows over 10 KiB (config D's U[8,512] B keys): two waves per window
+    if constexpr (OUT != kOutProbe)
+      if (SHFHB_SPAN_PINGPONG && need > 10240.0 + kSpanPad)
+        return launch_var_span_pingpong<OUT>(bytes, offsets, off_base, n, seed, sink, st);
     if (need >= (double)kSpanAlloc)
       return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, kSpanAlloc);
     const uint32_t w = (uint32_t)need;

@@ -21,8 +21,13 @@ constexpr uint64_t kN2 = 0x38495ab5ull;          // murmurhash3.c:103
 constexpr uint64_t kF1 = 0xff51afd7ed558ccdull;  // murmurhash3.c:65
 constexpr uint64_t kF2 = 0xc4ceb9fe1a85ec53ull;  // murmurhash3.c:67
 
+typedef uint32_t u32x2_mix __attribute__((ext_vector_type(2)));
+
+// {lo, hi} -> u64 as a register pair. Written as a bit cast: the shift-or form
+// lets the compiler split a later 64-bit add into two (one per half, plus a
+// zeroed register each), e.g. in rotl64(...) + h2.
 __device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
-  return (uint64_t)lo | ((uint64_t)hi << 32);
+  return __builtin_bit_cast(uint64_t, (u32x2_mix){lo, hi});
 }
 
 // Rotates as two v_alignbit_b32 and `x * 5` as one v_lshl_add_u64, with the
