@@ -711,6 +711,7 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
 #define SHFHB_SPAN_PINGPONG 1  // k_span_pp for variable-length windows over 10 KiB
 #endif
 
+
 // hash_lds with one unaligned ds_read_b128 per block instead of dword reads
 // funnel-shifted by v_alignbyte_b32 (gfx950 runs LDS accesses in unaligned
 // mode; hipcc emits ds_read_b128 for an align-1 vector LDS load).
@@ -727,8 +728,9 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
   State s{seed, seed};
   // software pipeline: block j's chain beside block j+1's mixes and block j+2's read
   // (the compiler folds this loop-carried read into one read at the point of
-  // use; forcing it a block ahead -- an opaque copy plus a sched_barrier --
-  // measured no faster, profiles/r2/ab_span/)
+  // use; forcing it a block ahead, or a two-block-deep pipeline with block
+  // j+2's mixes beside block j's chain, measured no faster in k_span or
+  // k_span_pp: profiles/r2/ab_span/ab_pipe, ab_deep)
   u32x4 cur = lds_read16(lds, p);
   u32x4 nxt = lds_read16(lds, p + 16u);
   uint64_t m1 = mix_k1(pack64(cur.x, cur.y)), m2 = mix_k2(pack64(cur.z, cur.w));
