@@ -232,6 +232,68 @@ SHF_HB_API int shf_probe_batch_fixed_kernel_async(const shf_row_index *index, co
                                                   shf_hash128 *d_hashes, shf_probe *d_probe, int kernel,
                                                   void *hip_stream);
 
+/* ---- tab part / shrink copy ------------------------------
+ *
+ * The two places the reference re-packs a tab's key,value data:
+ *   shf_tab_part()   /root/reference/src/shf.c:722-779: a full tab's window map
+ *                    sends every second tab2 naming it to a new tab (:683-692,
+ *                    shf_tab_part_redirect below), every ref whose tab2 now
+ *                    names the new tab is copied into it, then
+ *   shf_tab_shrink() /root/reference/src/shf.c:678-720: the old tab is
+ *                    re-created holding only its remaining refs' data.
+ * A job takes one tab image (the bytes of a tab file: SHF_TAB_MMAP header,
+ * 512 rows x 16 refs, data; shf.private.h:48-68) and writes the image of the
+ * shrunk tab ("keep": refs that stay) and, for a part, of the new tab
+ * ("move": refs whose tab2 the job's map sends to tab_new), byte for byte what
+ * the reference's part / shrink leave in those files: header, all rows (a ref
+ * not copied is 0), records appended in row/ref order. Bytes of an output past
+ * its tab_used are not written.
+ *
+ * Reference quirks kept as they are: tab_refs_used counts each copied ref
+ * twice (SHF_TAB_APPEND, shf.c:608, and SHF_TAB_REF_COPY, :651); the
+ * SHF_DATA_TYPE byte at each copied record has an uninitialised `extended`
+ * bit (shf.c:593-596), so the reference writes 0x3e or 0xbe depending on its
+ * stack: the job names the byte to write per output. */
+#define SHF_TAB_NONE 0xffffu /* tab_new of a shrink-only job */
+
+typedef struct shf_tab_job {
+    uint64_t src;       /* byte offset of the source tab image in the source buffer (8-B aligned) */
+    uint64_t src_len;   /* its bytes (the tab file's size; at least its tab_used) */
+    uint64_t keep;      /* byte offset of the keep (shrunk tab) output image in the output buffer (8-B aligned) */
+    uint64_t move;      /* byte offset of the move (new tab) output image (8-B aligned); unused if tab_new is NONE */
+    uint64_t cap;       /* bytes available at keep and at move each (>= 65560) */
+    uint32_t map;       /* index of this job's 2048-entry tab2 -> tab map (after the redirect) */
+    uint16_t tab_new;   /* the new tab's number, or SHF_TAB_NONE: shrink only */
+    uint8_t keep_type;  /* SHF_DATA_TYPE byte written at each record copied to keep (0x3e: key and value STR32) */
+    uint8_t move_type;  /* ... copied to move */
+    int32_t status;     /* out: SHF_HB_OK, or SHF_HB_ERR_ARG (out of range, corrupt record, output too small) */
+    uint32_t reserved;
+} shf_tab_job;
+
+typedef struct shf_tab_params {
+    uint32_t fixed;              /* nonzero: a fixed-length store (SHF.is_fixed_key_val_len) */
+    uint32_t fixed_key_len;      /* its key and value lengths (shf_set_is_fixed_len) */
+    uint32_t fixed_val_len;
+    uint32_t data_needed_factor; /* the tab growth factor (shf_set_data_need_factor; 0 = the default 1) */
+} shf_tab_params;
+
+/* Device-resident: every buffer in HBM (jobs too: their status is written
+ * back there). src_bytes / dst_bytes / n_maps bound what the jobs may name. */
+SHF_HB_API int shf_tab_copy_batch_async(const void *d_src, uint64_t src_bytes, void *d_dst, uint64_t dst_bytes,
+                                        shf_tab_job *d_jobs, uint32_t n_jobs, const uint16_t *d_maps,
+                                        uint32_t n_maps, const shf_tab_params *params, void *hip_stream);
+/* Synchronous: mem = SHF_HASH_MEM_DEVICE (every buffer in HBM) or
+ * SHF_HASH_MEM_HOST (host buffers, copied through the device; dst keeps the
+ * bytes the copy does not write). Returns SHF_HB_ERR_ARG if any job failed
+ * (see its status). */
+SHF_HB_API int shf_tab_copy_batch(const void *src, uint64_t src_bytes, void *dst, uint64_t dst_bytes,
+                                  shf_tab_job *jobs, uint32_t n_jobs, const uint16_t *maps, uint32_t n_maps,
+                                  const shf_tab_params *params, int mem);
+/* shf_tab_part()'s redirect of a window's 2048-entry tab2 -> tab map (host
+ * memory, shf.c:683-692): of the entries naming tab_old, every second one
+ * (the 2nd, 4th, ...) now names tab_new. */
+SHF_HB_API int shf_tab_part_redirect(uint16_t *map, uint32_t tab_old, uint32_t tab_new);
+
 /* ---- status of asynchronous variable-length calls -------------------------
  * Waits for hip_stream (NULL = the null stream), then returns SHF_HB_ERR_ARG if
  * any asynchronous variable-length call (hashing, UID parts or probe) that

@@ -13,6 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_shf.so")
 
+# SHF_DATA_TYPE byte of copied records as the reference's build writes them
+# (oracle/tab_oracle.h): 0x3e in shf_tab_shrink()'s copies, 0xbe in shf_tab_part()'s
+TAB_KEEP_TYPE = 0x3E
+TAB_MOVE_TYPE = 0xBE
+
 
 def _ensure_built():
     if not os.path.exists(ORACLE_SO):
@@ -31,6 +36,9 @@ class Oracle:
         lib.oracle_uid_parts_batch.argtypes = [vp, u64, vp]
         lib.oracle_smhasher_verification.restype = u32
         lib.oracle_probe.argtypes = [vp, u64, vp, vp, u64, vp]
+        lib.oracle_tab_split.argtypes = [vp, u64, vp, u32, ctypes.c_int, u32, u32, u32, u32, u32, vp, u64, vp, u64]
+        lib.oracle_tab_split.restype = ctypes.c_int
+        lib.oracle_tab_part_redirect.argtypes = [vp, u32, u32]
         self.lib = lib
 
     def hash(self, key: bytes, seed=12345):
@@ -79,6 +87,29 @@ class Oracle:
         self.lib.oracle_probe(hashes.ctypes.data, n, tab_slot.ctypes.data, rows.ctypes.data, n_slots, out.ctypes.data)
         return out
 
+    def tab_part_redirect(self, tab_map, tab_old, tab_new):
+        """shf_tab_part()'s redirect of a window's 2048-entry tab2 -> tab map (a new array)."""
+        m = np.array(tab_map, dtype=np.uint16)
+        self.lib.oracle_tab_part_redirect(m.ctypes.data, tab_old, tab_new)
+        return m
+
+    def tab_split(self, src, tab_map, tab_new=0xFFFF, fixed=0, key_len=0, val_len=0, factor=1, cap=None,
+                  keep_type=TAB_KEEP_TYPE, move_type=TAB_MOVE_TYPE):
+        """(keep, move) tab images: the part/shrink copy of tab image `src`
+        (tab_new = 0xFFFF: shrink only, move is None). keep_type / move_type:
+        the data-type byte of the copies (oracle/tab_oracle.h)."""
+        src = np.ascontiguousarray(src, dtype=np.uint8)
+        m = np.ascontiguousarray(tab_map, dtype=np.uint16)
+        cap = int(cap or src.size)
+        keep = np.zeros(cap, dtype=np.uint8)
+        move = np.zeros(cap, dtype=np.uint8) if tab_new != 0xFFFF else None
+        rc = self.lib.oracle_tab_split(src.ctypes.data, src.size, m.ctypes.data, tab_new, int(fixed), key_len, val_len,
+                                       factor, keep_type, move_type, keep.ctypes.data, cap,
+                                       move.ctypes.data if move is not None else None, cap if move is not None else 0)
+        if rc:
+            raise ValueError("oracle_tab_split: output does not fit")
+        return keep, move
+
     def smhasher(self):
         return self.lib.oracle_smhasher_verification()
 
@@ -107,6 +138,9 @@ def reference_lib():
     lib.ref_store_get_plain.restype = ctypes.c_int64
     lib.ref_store_get_probed.argtypes = [vp, vp, vp, u64, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)]
     lib.ref_store_get_probed.restype = ctypes.c_int64
+    lib.ref_part_capture.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, u32, u32, u32, u32,
+                                     ctypes.c_char_p]
+    lib.ref_part_capture.restype = ctypes.c_int64
     return lib
 
 
@@ -134,3 +168,38 @@ def reference_probe_fixture(data, offsets, n_put, n_query=None, max_slots=4096, 
     if slots < 0:
         raise RuntimeError("ref_probe_fixture failed (%d)" % slots)
     return uids, tab_slot, rows[: slots * 65536].copy()
+
+
+def reference_part_capture(data, offsets, fixed_key_len=0, fixed_val_len=0, factor=1, max_caps=2, folder=None):
+    """The reference's own shf_tab_part() (+ its shf_tab_shrink()), captured by
+    oracle/ref_export.c ref_part_capture(): keys put one by one into a fresh
+    store; for each put that parted a tab, the tab file before, both tab files
+    after, and the window's tab map before/after. Returns a list of dicts."""
+    import tempfile
+    import uuid
+
+    lib = reference_lib()
+    if lib is None:
+        raise RuntimeError("oracle/_ref/libref_shf.so not built")
+    data = np.ascontiguousarray(data).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    base = folder or ("/dev/shm" if os.path.isdir("/dev/shm") else None)
+    with tempfile.TemporaryDirectory(dir=base) as store, tempfile.TemporaryDirectory(dir=base) as out:
+        name = "part" + uuid.uuid4().hex[:8]
+        caps = lib.ref_part_capture(store.encode(), name.encode(), data.ctypes.data, offsets.ctypes.data, n,
+                                    fixed_key_len, fixed_val_len, factor, max_caps, out.encode())
+        if caps < 0:
+            raise RuntimeError("ref_part_capture failed (%d)" % caps)
+        res = []
+        for c in range(caps):
+            rd = lambda ext: np.fromfile(os.path.join(out, "cap%d.%s" % (c, ext)), dtype=np.uint8)
+            meta = rd("meta")
+            m32 = meta[:36].view(np.uint32)
+            maps = meta[36:].view(np.uint16)
+            res.append({"win": int(m32[0]), "tab_old": int(m32[1]), "tab_new": int(m32[2]), "uid": int(m32[3]),
+                        "key": int(m32[4]), "fixed": int(m32[5]), "fixed_key_len": int(m32[6]),
+                        "fixed_val_len": int(m32[7]), "factor": int(m32[8]), "map_before": maps[:2048].copy(),
+                        "map_after": maps[2048:].copy(), "before": rd("before"), "old": rd("old"),
+                        "new": rd("new")})
+        return res

@@ -182,3 +182,114 @@ int64_t ref_store_get_probed(SHF *shf, const uint8_t *bytes, const uint64_t *off
     if (fast) *fast = f;
     return good;
 }
+
+/* ---- f4: shf_tab_part() / shf_tab_shrink() captured from the reference ------
+ * Puts keys [0, n) one by one with the reference's own shf_make_hash() +
+ * shf_put_key_val() (value: the key index, 8 bytes; in a fixed-length store
+ * fixed_val_len bytes of it, repeated). Before every put it reads the key's
+ * row from its tab file: a put into a full row parts that tab (shf.c:829-834 ->
+ * shf_tab_part() at :722-779, which ends in shf_tab_shrink() at :678-720).
+ * For up to max_caps such puts (and only those that parted exactly once) it
+ * writes into out_dir:
+ *   cap<c>.before  tab_old's file before the put
+ *   cap<c>.old     tab_old's file after the put (re-created by the shrink)
+ *   cap<c>.new     tab_new's file after the put
+ *   cap<c>.meta    u32 {win, tab_old, tab_new, shf_uid of the put, key index,
+ *                  fixed, fixed_key_len, fixed_val_len, data_needed_factor},
+ *                  then the window's 2048 u16 tab2 -> tab map before and after.
+ * fixed_key_len > 0 makes a fixed-length store (shf_set_is_fixed_len); the
+ * data-needed factor is the reference's tab growth factor (shf.c:565).
+ * Returns the number of captures, or < 0 (-3 store, -4 I/O). */
+static int ref_copy_file(const char *from, const char *to)
+{
+    const int in = open(from, O_RDONLY);
+    if (in < 0) return -1;
+    const int out = open(to, O_WRONLY | O_CREAT | O_TRUNC, 0600);
+    if (out < 0) { close(in); return -1; }
+    char buf[1 << 16];
+    ssize_t got;
+    int rc = 0;
+    while ((got = read(in, buf, sizeof buf)) > 0)
+        if (write(out, buf, (size_t)got) != got) { rc = -1; break; }
+    if (got < 0) rc = -1;
+    close(in);
+    close(out);
+    return rc;
+}
+
+int64_t ref_part_capture(const char *folder, const char *name, const uint8_t *bytes, const uint64_t *offsets,
+                         uint64_t n, uint32_t fixed_key_len, uint32_t fixed_val_len, uint32_t factor,
+                         uint32_t max_caps, const char *out_dir)
+{
+    shf_init();
+    SHF *shf = shf_attach(folder, name, 0);
+    if (!shf) return -3;
+    shf_set_is_lockable(shf, 0);
+    if (fixed_key_len) shf_set_is_fixed_len(shf, fixed_key_len, fixed_val_len);
+    shf_set_data_need_factor(factor ? factor : 1);
+    char val[4096];
+    int64_t caps = 0;
+    for (uint64_t i = 0; i < n && caps < (int64_t)max_caps; ++i) {
+        const char *key = (const char *)bytes + offsets[i];
+        const uint32_t key_len = (uint32_t)(offsets[i + 1] - offsets[i]);
+        uint32_t val_len = sizeof(i);
+        if (fixed_key_len) {
+            val_len = fixed_val_len;
+            for (uint32_t b = 0; b < val_len && b < sizeof val; ++b) val[b] = ((const char *)&i)[b % sizeof(i)];
+        } else {
+            memcpy(val, &i, sizeof(i));
+        }
+        shf_make_hash(key, key_len);
+        const uint32_t win = shf_hash.u16[0] % SHF_WINS_PER_SHF;
+        const uint32_t tab2 = shf_hash.u16[1] % SHF_TABS_PER_WIN;
+        const uint32_t row = shf_hash.u16[2] % SHF_ROWS_PER_TAB;
+        volatile SHF_WIN_MMAP *w = &shf->shf_mmap->wins[win];
+        const uint32_t tab_old = w->tabs[tab2].tab;
+        const uint32_t used0 = w->tabs_used;
+        char file_old[512];
+        snprintf(file_old, sizeof file_old, "%s/%s.shf/%03u/%04u.tab", shf->path, shf->name, win, tab_old);
+        SHF_ROW_MMAP r;
+        int full = 0;
+        {
+            const int fd = open(file_old, O_RDONLY);
+            if (fd < 0) { (void)shf_del(shf); return -4; }
+            const ssize_t got = pread(fd, &r, sizeof r, offsetof(SHF_TAB_MMAP, row) + row * sizeof r);
+            close(fd);
+            if (got != (ssize_t)sizeof r) { (void)shf_del(shf); return -4; }
+            full = 1;
+            for (uint32_t k = 0; k < SHF_REFS_PER_ROW; ++k) full &= r.ref[k].pos != 0;
+        }
+        char path[1024];
+        uint16_t map_before[SHF_TABS_PER_WIN];
+        if (full) {
+            for (uint32_t t2 = 0; t2 < SHF_TABS_PER_WIN; ++t2) map_before[t2] = w->tabs[t2].tab;
+            snprintf(path, sizeof path, "%s/cap%lld.before", out_dir, (long long)caps);
+            if (ref_copy_file(file_old, path)) { (void)shf_del(shf); return -4; }
+        }
+        if (shf_put_key_val(shf, val, val_len) != SHF_RET_KEY_PUT) { (void)shf_del(shf); return -3; }
+        if (!full || w->tabs_used != used0 + 1) continue;  /* no part, or more than one */
+        const uint32_t tab_new = used0;
+        char file_new[512];
+        snprintf(file_new, sizeof file_new, "%s/%s.shf/%03u/%04u.tab", shf->path, shf->name, win, tab_new);
+        snprintf(path, sizeof path, "%s/cap%lld.old", out_dir, (long long)caps);
+        if (ref_copy_file(file_old, path)) { (void)shf_del(shf); return -4; }
+        snprintf(path, sizeof path, "%s/cap%lld.new", out_dir, (long long)caps);
+        if (ref_copy_file(file_new, path)) { (void)shf_del(shf); return -4; }
+        uint32_t meta[9] = {win, tab_old, tab_new, shf_uid, (uint32_t)i, fixed_key_len ? 1u : 0u, fixed_key_len,
+                            fixed_val_len, factor ? factor : 1u};
+        uint16_t map_after[SHF_TABS_PER_WIN];
+        for (uint32_t t2 = 0; t2 < SHF_TABS_PER_WIN; ++t2) map_after[t2] = w->tabs[t2].tab;
+        snprintf(path, sizeof path, "%s/cap%lld.meta", out_dir, (long long)caps);
+        const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0600);
+        if (fd < 0) { (void)shf_del(shf); return -4; }
+        const int ok = write(fd, meta, sizeof meta) == (ssize_t)sizeof meta &&
+                       write(fd, map_before, sizeof map_before) == (ssize_t)sizeof map_before &&
+                       write(fd, map_after, sizeof map_after) == (ssize_t)sizeof map_after;
+        close(fd);
+        if (!ok) { (void)shf_del(shf); return -4; }
+        ++caps;
+    }
+    shf_set_data_need_factor(1);
+    (void)shf_del(shf);
+    return caps;
+}

@@ -90,6 +90,9 @@ _SIGS = {
     "shf_probe_batch_var": [_VP, _VP, _VP, _U64, _U32, _VP, _VP, _INT],
     "shf_probe_batch_fixed_kernel_async": [_VP, _VP, _U32, _U64, _U32, _VP, _VP, _INT, _VP],
     "shf_hash_batch_status": [_VP],
+    "shf_tab_copy_batch_async": [_VP, _U64, _VP, _U64, _VP, _U32, _VP, _U32, _VP, _VP],
+    "shf_tab_copy_batch": [_VP, _U64, _VP, _U64, _VP, _U32, _VP, _U32, _VP, _INT],
+    "shf_tab_part_redirect": [_VP, _U32, _U32],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
@@ -506,6 +509,97 @@ def hash_var_host(data, offsets, seed=SEED, n_devices=None):
                                           n_devices)
         _check(rc, "shf_hash_batch_var_multi")
     return out
+
+
+# ---------------------------------------------------------------------------
+# Tab part / shrink copy (include/shf_hash_batch.h)
+# ---------------------------------------------------------------------------
+TAB_NONE = 0xFFFF
+TAB_DATA = 24 + 512 * 16 * 8  # offsetof(SHF_TAB_MMAP, data)
+
+
+class TabJob(ctypes.Structure):
+    _fields_ = [("src", _U64), ("src_len", _U64), ("keep", _U64), ("move", _U64), ("cap", _U64), ("map", _U32),
+                ("tab_new", ctypes.c_uint16), ("keep_type", ctypes.c_uint8), ("move_type", ctypes.c_uint8),
+                ("status", ctypes.c_int32), ("reserved", _U32)]
+
+
+class TabParams(ctypes.Structure):
+    _fields_ = [("fixed", _U32), ("fixed_key_len", _U32), ("fixed_val_len", _U32), ("data_needed_factor", _U32)]
+
+
+def tab_part_redirect(tab_map, tab_old, tab_new):
+    """shf_tab_part()'s map redirect (a new uint16 array)."""
+    m = np.array(tab_map, dtype=np.uint16)
+    _check(load().shf_tab_part_redirect(m.ctypes.data, tab_old, tab_new), "shf_tab_part_redirect")
+    return m
+
+
+def tab_copy(images, maps=None, tab_new=None, fixed=0, key_len=0, val_len=0, factor=1, keep_type=0x3E,
+             move_type=0x3E, cap=None, device=None):
+    """Part / shrink copy of a batch of tab images on the GPU.
+
+    images: list of uint8 numpy tab images; maps: list of 2048-entry uint16
+    maps (after the redirect) per image (None for shrink-only);
+    tab_new: list of new-tab numbers (TAB_NONE: shrink). Returns a list of
+    (keep, move) uint8 numpy images of `cap` bytes each (zero past tab_used;
+    move None for a shrink). keep_type / move_type: int or per-job lists.
+    Device-resident: the images are packed into one HBM buffer and copied back.
+    """
+    import torch
+
+    n = len(images)
+    tab_new = [TAB_NONE] * n if tab_new is None else list(tab_new)
+    kt = keep_type if isinstance(keep_type, (list, tuple)) else [keep_type] * n
+    mt = move_type if isinstance(move_type, (list, tuple)) else [move_type] * n
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    al = lambda x: (x + 4095) // 4096 * 4096
+    caps = [al(int(cap or img.size)) for img in images]
+    src_off, off = [], 0
+    for img in images:
+        src_off.append(off)
+        off += al(img.size)
+    src = torch.zeros(max(off, 8), dtype=torch.uint8, device=dev)
+    for o, img in zip(src_off, images):
+        src[o:o + img.size] = torch.from_numpy(np.ascontiguousarray(img, dtype=np.uint8)).to(dev)
+    jobs = (TabJob * n)()
+    doff = 0
+    for i in range(n):
+        j = jobs[i]
+        j.src, j.src_len, j.cap, j.map = src_off[i], images[i].size, caps[i], i if maps is not None else 0
+        j.keep = doff
+        doff += caps[i]
+        j.tab_new = tab_new[i]
+        if tab_new[i] != TAB_NONE:
+            j.move = doff
+            doff += caps[i]
+        j.keep_type, j.move_type, j.status = kt[i], mt[i], 1
+    dst = torch.zeros(max(doff, 8), dtype=torch.uint8, device=dev)
+    d_jobs = torch.from_numpy(np.frombuffer(bytes(jobs), dtype=np.uint8).copy()).to(dev)
+    d_maps = None
+    if maps is not None:
+        d_maps = torch.from_numpy(np.ascontiguousarray(np.stack([np.asarray(m, np.uint16) for m in maps]))
+                                  .view(np.int16)).to(dev)
+    prm = TabParams(int(bool(fixed)), key_len, val_len, factor)
+    with _on(src):
+        rc = load().shf_tab_copy_batch_async(
+            ctypes.c_void_p(src.data_ptr()), src.numel(), ctypes.c_void_p(dst.data_ptr()), dst.numel(),
+            ctypes.c_void_p(d_jobs.data_ptr()), n, ctypes.c_void_p(d_maps.data_ptr() if d_maps is not None else 0),
+            n if d_maps is not None else 0, ctypes.byref(prm), _stream_handle(None))
+    _check(rc, "shf_tab_copy_batch_async")
+    torch.cuda.synchronize(dev)
+    done = (TabJob * n).from_buffer_copy(d_jobs.cpu().numpy().tobytes())
+    bad = [i for i in range(n) if done[i].status != OK]
+    if bad:
+        raise ShfHashBatchError(ERR_ARG, "shf_tab_copy_batch_async (jobs %s)" % bad[:8])
+    out_h = dst.cpu().numpy()
+    res = []
+    for i in range(n):
+        j = jobs[i]
+        keep = out_h[j.keep:j.keep + caps[i]].copy()
+        move = out_h[j.move:j.move + caps[i]].copy() if tab_new[i] != TAB_NONE else None
+        res.append((keep, move))
+    return res
 
 
 def device_count():

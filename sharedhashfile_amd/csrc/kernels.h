@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/shf_hash_batch.h"
+
 namespace shfhb {
 
 // kOutHash: 16-B SHF_HASH records; kOutUid: 8-B packed UID parts;
@@ -42,5 +44,10 @@ hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_b
 
 // Row pre-probe of precomputed hashes (n x 16 B on device) into sink.out.
 hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st);
+
+// Tab part / shrink copy (tab_copy.hip): one workgroup per job, every pointer on device.
+hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint64_t dst_bytes, shf_tab_job* jobs,
+                            uint32_t n_jobs, const uint16_t* maps, uint32_t n_maps, const shf_tab_params& prm,
+                            hipStream_t st);
 
 }  // namespace shfhb

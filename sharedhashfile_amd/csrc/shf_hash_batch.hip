@@ -946,6 +946,69 @@ int shf_probe_batch_hashes_async(const shf_row_index* index, const shf_hash128* 
   return SHF_HB_OK;
 }
 
+int shf_tab_copy_batch_async(const void* d_src, uint64_t src_bytes, void* d_dst, uint64_t dst_bytes,
+                             shf_tab_job* d_jobs, uint32_t n_jobs, const uint16_t* d_maps, uint32_t n_maps,
+                             const shf_tab_params* params, void* hip_stream) {
+  if (n_jobs == 0) return SHF_HB_OK;
+  if (!d_src || !d_dst || !d_jobs || !params) return SHF_HB_ERR_ARG;
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  HB_TRY(shfhb::launch_tab_split(d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_maps, d_maps ? n_maps : 0,
+                                 *params, (hipStream_t)hip_stream));
+  return SHF_HB_OK;
+}
+
+int shf_tab_copy_batch(const void* src, uint64_t src_bytes, void* dst, uint64_t dst_bytes, shf_tab_job* jobs,
+                       uint32_t n_jobs, const uint16_t* maps, uint32_t n_maps, const shf_tab_params* params, int mem) {
+  if (n_jobs == 0) return SHF_HB_OK;
+  if (!src || !dst || !jobs || !params || (mem != SHF_HASH_MEM_DEVICE && mem != SHF_HASH_MEM_HOST))
+    return SHF_HB_ERR_ARG;
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  hipStream_t st = c->st[0];
+  const size_t job_bytes = (size_t)n_jobs * sizeof(shf_tab_job), map_bytes = (size_t)n_maps * 2048u * 2u;
+  if (mem == SHF_HASH_MEM_DEVICE) {
+    HB_TRY(shfhb::launch_tab_split(src, src_bytes, dst, dst_bytes, jobs, n_jobs, maps, maps ? n_maps : 0, *params, st));
+    HB_TRY(hipStreamSynchronize(st));
+    std::vector<shf_tab_job> h(n_jobs);
+    HB_TRY(hipMemcpy(h.data(), jobs, job_bytes, hipMemcpyDeviceToHost));
+    for (const auto& j : h)
+      if (j.status != SHF_HB_OK) return SHF_HB_ERR_ARG;
+    return SHF_HB_OK;
+  }
+  // host buffers: through temporary device copies (dst too, so bytes the copy does not write keep their values)
+  TmpDevBuf d_src, d_dst, d_jobs, d_maps;
+  HB_TRY(hipMalloc(&d_src.p, src_bytes ? src_bytes : 1));
+  HB_TRY(hipMalloc(&d_dst.p, dst_bytes ? dst_bytes : 1));
+  HB_TRY(hipMalloc(&d_jobs.p, job_bytes));
+  if (maps && n_maps) HB_TRY(hipMalloc(&d_maps.p, map_bytes));
+  HB_TRY(hipMemcpyAsync(d_src.p, src, src_bytes, hipMemcpyHostToDevice, st));
+  HB_TRY(hipMemcpyAsync(d_dst.p, dst, dst_bytes, hipMemcpyHostToDevice, st));
+  HB_TRY(hipMemcpyAsync(d_jobs.p, jobs, job_bytes, hipMemcpyHostToDevice, st));
+  if (d_maps.p) HB_TRY(hipMemcpyAsync(d_maps.p, maps, map_bytes, hipMemcpyHostToDevice, st));
+  HB_TRY(shfhb::launch_tab_split(d_src.p, src_bytes, d_dst.p, dst_bytes, (shf_tab_job*)d_jobs.p, n_jobs,
+                                 (const uint16_t*)d_maps.p, d_maps.p ? n_maps : 0, *params, st));
+  HB_TRY(hipMemcpyAsync(dst, d_dst.p, dst_bytes, hipMemcpyDeviceToHost, st));
+  HB_TRY(hipMemcpyAsync(jobs, d_jobs.p, job_bytes, hipMemcpyDeviceToHost, st));
+  HB_TRY(hipStreamSynchronize(st));
+  for (uint32_t i = 0; i < n_jobs; ++i)
+    if (jobs[i].status != SHF_HB_OK) return SHF_HB_ERR_ARG;
+  return SHF_HB_OK;
+}
+
+int shf_tab_part_redirect(uint16_t* map, uint32_t tab_old, uint32_t tab_new) {
+  if (!map || tab_old >= 2048u || tab_new >= 2048u || tab_old == tab_new) return SHF_HB_ERR_ARG;
+  bool second = false;  // shf.c:683-692: the 1st, 3rd, ... stay, the 2nd, 4th, ... move
+  for (uint32_t tab2 = 0; tab2 < 2048u; ++tab2) {
+    if (map[tab2] != tab_old) continue;
+    if (second) map[tab2] = (uint16_t)tab_new;
+    second = !second;
+  }
+  return SHF_HB_OK;
+}
+
 int shf_hash_batch_status(void* hip_stream) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);

@@ -144,6 +144,11 @@ def test_no_device_fails_loudly_not_on_cpu(hb):
     assert h.value is None
     with pytest.raises(hbmod.ShfHashBatchError):
         hbmod.RowIndex(4)
+    prm = hbmod.TabParams(0, 0, 0, 1)
+    jobs = (hbmod.TabJob * 1)()
+    img = np.zeros(70000, dtype=np.uint8)
+    assert lib.shf_tab_copy_batch(img.ctypes.data, img.size, img.ctypes.data, img.size, ctypes.addressof(jobs), 1,
+                                  None, 0, ctypes.byref(prm), hbmod.MEM_HOST) in (hbmod.ERR_NODEV, hbmod.ERR_HIP)
 
 
 def test_missing_library_raises(tmp_path):
@@ -169,3 +174,36 @@ def test_kernels_compile_without_scratch():
     assert p.returncode == 0, p.stderr
     scratch = [int(x) for x in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", p.stderr)]
     assert len(scratch) >= 10 and max(scratch) == 0, scratch
+
+
+def test_tab_part_redirect_on_the_host(hb, oracle):
+    """shf_tab_part_redirect is host code (no device needed): the oracle's
+    restatement of shf.c:683-692 on maps with 1-3 tabs."""
+    lib = hb.load()
+    rng = np.random.default_rng(9)
+    for tabs in (1, 2, 3):
+        m = (np.arange(2048) % tabs).astype(np.uint16)
+        rng.shuffle(m)
+        for old in range(tabs):
+            got = hbmod.tab_part_redirect(m, old, tabs)
+            assert np.array_equal(got, oracle.tab_part_redirect(m, old, tabs))
+            assert (got == tabs).sum() == (m == old).sum() // 2
+    m = np.zeros(2048, dtype=np.uint16)
+    assert lib.shf_tab_part_redirect(None, 0, 1) == hbmod.ERR_ARG
+    assert lib.shf_tab_part_redirect(m.ctypes.data, 3, 3) == hbmod.ERR_ARG
+    assert lib.shf_tab_part_redirect(m.ctypes.data, 0, 2048) == hbmod.ERR_ARG
+
+
+def test_tab_copy_argument_validation_needs_no_device(hb):
+    lib = hb.load()
+    prm = hbmod.TabParams(0, 0, 0, 1)
+    buf = np.zeros(16, dtype=np.uint8)
+    assert lib.shf_tab_copy_batch(None, 0, None, 0, None, 0, None, 0, None, hbmod.MEM_HOST) == hbmod.OK  # no jobs
+    assert lib.shf_tab_copy_batch(None, 16, buf.ctypes.data, 16, buf.ctypes.data, 1, None, 0, ctypes.byref(prm),
+                                  hbmod.MEM_HOST) == hbmod.ERR_ARG
+    assert lib.shf_tab_copy_batch(buf.ctypes.data, 16, buf.ctypes.data, 16, buf.ctypes.data, 1, None, 0, None,
+                                  hbmod.MEM_HOST) == hbmod.ERR_ARG
+    assert lib.shf_tab_copy_batch(buf.ctypes.data, 16, buf.ctypes.data, 16, buf.ctypes.data, 1, None, 0,
+                                  ctypes.byref(prm), 7) == hbmod.ERR_ARG
+    assert lib.shf_tab_copy_batch_async(None, 0, buf.ctypes.data, 16, buf.ctypes.data, 1, None, 0,
+                                        ctypes.byref(prm), None) == hbmod.ERR_ARG

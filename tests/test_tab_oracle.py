@@ -1,0 +1,81 @@
+"""The f4 oracle (shf_tab_part() / shf_tab_shrink() copy,
+/root/reference/src/shf.c:633-779) pinned to the reference's own tab files.
+
+* tests/golden/tab_part_fixture.npz (tests/golden/make_tab_golden.py): a tab
+  parted by the reference, before and after, variable- and fixed-length stores,
+  data-needed factors 1 and 3;
+* where oracle/_ref exists, more parts captured live from the reference (key
+  lengths 4-200 B, factors 1-3), and shf_tab_part()'s map redirect.
+
+The comparison (tests/tabcheck.py) is byte for byte: header, all 512 rows and
+the data, except the one record and ref the parting put adds afterwards.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import tabcheck
+from oracle.oracle_py import reference_lib
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tab_part_fixture.npz")
+
+
+def fixture_caps():
+    with np.load(GOLDEN, allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    caps = []
+    for name in ("c0", "c1"):
+        m = d[name + "_meta"]
+        caps.append({"win": int(m[0]), "tab_old": int(m[1]), "tab_new": int(m[2]), "uid": int(m[3]),
+                     "key": int(m[4]), "fixed": int(m[5]), "fixed_key_len": int(m[6]), "fixed_val_len": int(m[7]),
+                     "factor": int(m[8]), "put_key_len": int(m[9]), "before": d[name + "_before"],
+                     "old": d[name + "_old"], "new": d[name + "_new"], "map_before": d[name + "_map_before"],
+                     "map_after": d[name + "_map_after"]})
+    return caps
+
+
+def oracle_part(oracle, cap):
+    m = oracle.tab_part_redirect(cap["map_before"], cap["tab_old"], cap["tab_new"])
+    kt, mt = tabcheck.observed_types(cap)
+    return m, oracle.tab_split(cap["before"], m, cap["tab_new"], cap["fixed"], cap["fixed_key_len"],
+                               cap["fixed_val_len"], cap["factor"], keep_type=kt, move_type=mt)
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_oracle_part_matches_reference_fixture(oracle, i):
+    cap = fixture_caps()[i]
+    m, (keep, move) = oracle_part(oracle, cap)
+    assert np.array_equal(m, cap["map_after"])  # shf.c:683-692
+    tabcheck.check_capture(cap, keep, move, cap["put_key_len"])
+
+
+def test_oracle_shrink_is_a_part_with_nothing_moving(oracle):
+    cap = fixture_caps()[0]
+    m = oracle.tab_part_redirect(cap["map_before"], cap["tab_old"], cap["tab_new"])
+    keep, move = oracle.tab_split(cap["before"], m, cap["tab_new"])
+    shrunk, none = oracle.tab_split(cap["before"], m)  # tab_new = none: every ref stays
+    assert none is None
+    h_k, h_m, h_s = tabcheck.hdr(keep), tabcheck.hdr(move), tabcheck.hdr(shrunk)
+    assert h_s[5] == h_k[5] + h_m[5] and h_s[2] == h_k[2] + h_m[2]
+    # a shrink of an already shrunk tab changes nothing
+    again, _ = oracle.tab_split(keep, m)
+    assert np.array_equal(again, keep)
+    # too small an output is refused
+    with pytest.raises(ValueError):
+        oracle.tab_split(cap["before"], m, cap["tab_new"], cap=70000)
+
+
+@pytest.mark.skipif(reference_lib() is None, reason="oracle/_ref not built")
+@pytest.mark.parametrize("lo,hi,fk,fv,fac", [(8, 40, 0, 0, 1), (16, 16, 16, 8, 3), (8, 200, 0, 0, 2),
+                                            (4, 12, 0, 0, 1), (32, 32, 32, 100, 1)])
+def test_oracle_part_matches_live_reference(oracle, lo, hi, fk, fv, fac):
+    from golden.make_tab_golden import window0_keys
+    from oracle.oracle_py import reference_part_capture
+
+    data, off = window0_keys(oracle, 3_000_000, lo, hi, 91 + lo + fv)
+    caps = reference_part_capture(data, off, fixed_key_len=fk, fixed_val_len=fv, factor=fac, max_caps=3)
+    assert len(caps) >= 2
+    for cap in caps:
+        _, (keep, move) = oracle_part(oracle, cap)
+        tabcheck.check_capture(cap, keep, move, int(off[cap["key"] + 1] - off[cap["key"]]))
