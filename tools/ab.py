@@ -50,6 +50,8 @@ def main():
     p.add_argument("--var-hi", type=int, default=512)
     p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
     p.add_argument("--sized", action="store_true", help="var: pass the batch byte count (sized-window API)")
+    p.add_argument("--warmup-s", type=float, default=1.0, help="untimed calls of every variant for this long first")
+    p.add_argument("--unchecked", action="append", default=[], help="variant whose results are not compared (ceilings)")
     p.add_argument("--prebuild", default="", help="build every name=-Dflags variant into this dir and exit")
     a = p.parse_args()
     if a.prebuild:
@@ -120,7 +122,7 @@ def main():
     torch.cuda.synchronize()
     ref = next(iter(outs.values()))
     for k, o in outs.items():
-        assert torch.equal(o, ref), "variant %s differs" % k
+        assert k in a.unchecked or torch.equal(o, ref), "variant %s differs" % k
     if a.copy_ref:  # a known-good streaming reference on the same device: bytes in == bytes out
         half = int(n * per_key) // 2
         src_c = torch.empty(half, dtype=torch.uint8, device=dev)
@@ -129,6 +131,11 @@ def main():
         outs["copy_ref"] = None
         call_orig = call
         call = lambda lib, out: (dst_c.copy_(src_c), 0)[1] if lib is None else call_orig(lib, out)
+    t_end = time.time() + a.warmup_s  # clocks and caches settle before the timed rounds
+    while time.time() < t_end:
+        for k, lib in libs.items():
+            call(lib, outs[k])
+        torch.cuda.synchronize()
     times = {k: [] for k in libs}
     for r in range(a.rounds):
         for k, lib in libs.items():
