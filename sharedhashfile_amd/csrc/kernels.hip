@@ -710,30 +710,6 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
 #ifndef SHFHB_SPAN_PINGPONG
 #define SHFHB_SPAN_PINGPONG 1  // k_span_pp for variable-length windows over 10 KiB
 #endif
-#ifndef SHFHB_SPAN_PC
-#define SHFHB_SPAN_PC 0  // k_span_pc (mix wave + chain wave per tile) instead of k_span_pp
-#endif
-#ifndef SHFHB_SPAN_PQ
-#define SHFHB_SPAN_PQ 0  // k_span_pq (persistent ping-pong) instead of k_span_pp
-#endif
-#ifndef SHFHB_PQ_EARLY
-#define SHFHB_PQ_EARLY 0  // k_span_pq: next span's loads issued before (1) or after (0) the hash
-#endif
-#ifndef SHFHB_PQ_GRID_MULT
-#define SHFHB_PQ_GRID_MULT 1  // k_span_pq grid = this many x the resident workgroups
-#endif
-#ifndef SHFHB_PP_PREFETCH_OFF
-#define SHFHB_PP_PREFETCH_OFF 0  // k_span_pp: tiles ahead whose offsets each wave pulls into L2 (0: none)
-#endif
-#ifndef SHFHB_PP_NOHASH
-#define SHFHB_PP_NOHASH 0
-#endif
-#ifndef SHFHB_PAIR_PREFETCH
-#define SHFHB_PAIR_PREFETCH 0
-#endif
-#ifndef SHFHB_SPAN_PAIR
-#define SHFHB_SPAN_PAIR 0  // k_span_pair (two keys per lane) where a 128-key span fits 40 KiB
-#endif
 
 
 // hash_lds with one unaligned ds_read_b128 per block instead of dword reads
@@ -1015,12 +991,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool staged = has && !bad && ti.span16 <= cap;
   u32x4 reg[PIECES];
   if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-#if SHFHB_PP_PREFETCH_OFF
-  // warm L2 with the offsets of the tile a generation of workgroups later
-  // (same XCD: workgroup ids deal round-robin over the 8 XCDs)
-  const uint64_t pk = (t + SHFHB_PP_PREFETCH_OFF) * 64u + lane;
-  const uint64_t pf = pk < n ? offsets[pk] : 0u;
-#endif
 #pragma unroll
   for (uint32_t phase = 0; phase < 2; ++phase) {
     if (wave == phase && staged) span_stage<PIECES>(span_lds, reg, ti.span16, lane);
@@ -1029,408 +999,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
       if (staged) {
         if (ti.valid) {
           const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-#if SHFHB_PP_NOHASH  // A/B only: the structure's ceiling without the hash (wrong results)
-          const u32x4 v = lds_read16(span_lds, p);
-          store_result<OUT>(sink, ti.key, State{pack64(v.x ^ ti.len, v.y), pack64(v.z, v.w)});
-#else
           store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, p, ti.len, seed));
-#endif
         }
       } else {
         span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-      }
-    }
-    __syncthreads();
-  }
-#if SHFHB_PP_PREFETCH_OFF
-  if (pf == 0x5eed5eed5eed5eedull && seed == 0x5eed5eedu) flag_bad_key(sink);  // keeps the prefetch alive
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// Persistent ping-pong span kernel (variable-length keys). k_span_pp's window
-// sits idle while its workgroup's offsets and then its spans are in flight:
-// two dependent HBM round trips per two tiles. Here a resident grid of
-// two-wave workgroups walks the tiles (wave w of workgroup b: tiles 2b + w,
-// + 2G, + 4G, ...), and each wave issues its next tile's span loads right
-// after its own hash (into the registers the hash no longer needs), with the
-// offsets of the tile after that already loaded a round earlier: the span
-// arrives while the other wave stages and hashes, so the window only waits
-// when one HBM latency exceeds a hash.
-// ---------------------------------------------------------------------------
-template <int OUT, int PIECES>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_span_pq(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint32_t seed, uint32_t cap, Sink sink) {
-  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint64_t ntiles = (n + 63) / 64;
-  const uint64_t stride = 2u * (uint64_t)gridDim.x;
-  // rounds of this workgroup: wave 0's tiles 2b, 2b + stride, ... below ntiles
-  const uint64_t first0 = 2u * (uint64_t)blockIdx.x;
-  const uint64_t rounds = first0 < ntiles ? (ntiles - first0 + stride - 1) / stride : 0u;
-  uint64_t t = first0 + wave;
-  // this wave's tile in flight: its offsets, its span tile, its registers
-  SpanRaw raw = span_load<true>(offsets, n, t, lane);  // keys past n: o0 = o1 = 0
-  bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-  SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-  bool staged = t < ntiles && !bad && ti.span16 <= cap;
-  u32x4 reg[PIECES];
-  if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-  SpanRaw raw_next = span_load<true>(offsets, n, t + stride, lane);
-  for (uint64_t r = 0; r < rounds; ++r) {
-#pragma unroll
-    for (uint32_t phase = 0; phase < 2; ++phase) {
-      if (wave == phase && staged) span_stage<PIECES>(span_lds, reg, ti.span16, lane);
-      __syncthreads();
-#if SHFHB_PQ_EARLY
-      // the staged span's registers are free: the next span flies during this hash
-      if (wave == phase) {
-        const bool cur = t < ntiles && staged && ti.valid;
-        const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base), len = ti.len;
-        const uint64_t key = ti.key;
-        if (t < ntiles && !staged) span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-        t += stride;
-        raw = raw_next;
-        bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-        ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-        staged = t < ntiles && !bad && ti.span16 <= cap;
-        if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-        raw_next = span_load<true>(offsets, n, t + stride, lane);
-        if (cur) store_result<OUT>(sink, key, hash_lds_u(span_lds, p, len, seed));
-      }
-#else
-      if (wave == phase) {
-        if (t < ntiles) {
-          if (staged) {
-            if (ti.valid) {
-              const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-              store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, p, ti.len, seed));
-            }
-          } else {
-            span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-          }
-        }
-        // next tile: its offsets arrived during this round; its span now flies
-        // while the other wave hashes. Then the offsets of the tile after it.
-        t += stride;
-        raw = raw_next;
-        bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-        ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-        staged = t < ntiles && !bad && ti.span16 <= cap;
-        if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-        raw_next = span_load<true>(offsets, n, t + stride, lane);
-      }
-#endif
-      __syncthreads();
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Producer/consumer span kernel (variable-length keys). k_span_pp's two-wave
-// workgroup and window, but both waves hash each staged tile: wave 1 mixes
-// the k1/k2 of every key's blocks (murmurhash3.c:97, :101; the independent,
-// multiply-heavy 60 % of a block) and writes them back over the block in the
-// window, C blocks per key per step; wave 0 runs the serial h1/h2 chain
-// (murmurhash3.c:98-99, :102-103) over the previous step's mixed blocks, then
-// the tail and fmix. One s_barrier per step. A tile's hash then takes about
-// the mix's share of k_span_pp's time instead of all of it, and the window
-// turns over sooner. Each wave loads both tiles' offsets (the second copy
-// hits L2) so no per-key table crosses through LDS.
-// ---------------------------------------------------------------------------
-#ifndef SHFHB_PC_CHUNK
-#define SHFHB_PC_CHUNK 4
-#endif
-__device__ __forceinline__ void lds_write16(uint32_t* lds, uint32_t byte, const u32x4& v) {
-  typedef __attribute__((address_space(3))) uint8_t lds_u8w;
-  typedef __attribute__((address_space(3))) u32x4_a1 lds_u32x4_a1w;
-  *(lds_u32x4_a1w*)((lds_u8w*)lds + byte) = v;
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m));
-  return __builtin_amdgcn_readfirstlane(v);
-}
-
-// One step of the mixing wave: blocks [C st, C st + C) of this lane's key
-// (nb full blocks at window byte p), mixed and written back in place.
-template <uint32_t C>
-__device__ __forceinline__ void pc_mix_step(uint32_t* lds, uint32_t p, uint32_t nb, uint32_t st) {
-  u32x4 v[C];
-#pragma unroll
-  for (uint32_t q = 0; q < C; ++q)
-    if (C * st + q < nb) v[q] = lds_read16(lds, p + 16u * (C * st + q));
-#pragma unroll
-  for (uint32_t q = 0; q < C; ++q)
-    if (C * st + q < nb) {
-      const uint64_t m1 = mix_k1(pack64(v[q].x, v[q].y)), m2 = mix_k2(pack64(v[q].z, v[q].w));
-      lds_write16(lds, p + 16u * (C * st + q), u32x4{(uint32_t)m1, (uint32_t)(m1 >> 32), (uint32_t)m2, (uint32_t)(m2 >> 32)});
-    }
-}
-
-// One step of the chaining wave: the blocks the mixing wave wrote a step earlier.
-template <uint32_t C>
-__device__ __forceinline__ void pc_chain_step(const uint32_t* lds, uint32_t p, uint32_t nb, uint32_t st, State& s) {
-  u32x4 v[C];
-#pragma unroll
-  for (uint32_t q = 0; q < C; ++q)
-    if (C * st + q < nb) v[q] = lds_read16(lds, p + 16u * (C * st + q));
-#pragma unroll
-  for (uint32_t q = 0; q < C; ++q)
-    if (C * st + q < nb) chain_block(s, pack64(v[q].x, v[q].y), pack64(v[q].z, v[q].w));
-}
-
-// Hash one staged tile with the other wave: `mixer` mixes, the other chains,
-// stores. Every wave of the workgroup calls it with the same (uniform) nbmax.
-template <int OUT, uint32_t C>
-__device__ __forceinline__ void pc_tile(uint32_t* lds, bool mixer, uint32_t p, uint32_t len, uint64_t key, uint64_t n,
-                                        uint32_t seed, const Sink& sink) {
-  const uint32_t nb = len >> 4;
-  const uint32_t steps = (wave_max_u32(nb) + C - 1) / C + 1;  // equal in both waves: same 64 lengths
-  State s{seed, seed};
-  for (uint32_t st = 0; st < steps; ++st) {
-    if (mixer) pc_mix_step<C>(lds, p, nb, st);
-    else if (st > 0) pc_chain_step<C>(lds, p, nb, st - 1, s);
-    __syncthreads();
-  }
-  if (!mixer && key < n) {
-    const uint32_t rem = len & 15u;
-    if (rem) {  // the tail's raw bytes (never mixed in place)
-      const u32x4 t = lds_read16(lds, p + 16u * nb);
-      const uint64_t t1 = pack64(t.x, t.y) & low_bytes_mask(rem);
-      const uint64_t t2 = rem > 8 ? (pack64(t.z, t.w) & low_bytes_mask(rem - 8)) : 0ull;
-      tail_block(s, t1, t2, rem);
-    }
-    finish(s, len);
-    store_result<OUT>(sink, key, s);
-  }
-}
-
-template <int OUT, int PIECES>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_span_pc(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint32_t seed, uint32_t cap, Sink sink) {
-  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
-  constexpr uint32_t C = SHFHB_PC_CHUNK;
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint64_t ntiles = (n + 63) / 64;
-  const uint64_t t0 = 2u * (uint64_t)blockIdx.x;  // phase q hashes tile t0 + q, fetched by wave q
-  // per tile, all a wave keeps while wave 1's span waits in registers: the
-  // lane's key's window byte and length (0 past n), and the tile's uniform span
-  uint32_t kp[2], kl[2];
-  uint64_t base[2];
-  uint32_t span16[2];
-  bool staged[2];
-#pragma unroll
-  for (uint32_t q = 0; q < 2; ++q) {
-    const SpanRaw raw = span_load<true>(offsets, n, t0 + q, lane);  // keys past n: o0 = o1 = 0
-    const bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-    const SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-    kp[q] = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-    kl[q] = ti.valid ? ti.len : 0u;
-    base[q] = ti.base;
-    span16[q] = ti.span16;
-    staged[q] = t0 + q < ntiles && !bad && ti.span16 <= cap;
-  }
-  const uint64_t k0 = t0 * 64u + lane, k1 = k0 + 64u;
-  // Separate code per wave, so that the compiler sees wave 0's span dead once
-  // staged; the stager of a tile mixes it, the other wave chains it. Barrier
-  // counts match: both waves step through each tile's longest key.
-  u32x4 reg[PIECES];
-  if (wave == 0) {
-    if (staged[0]) {
-      span_fetch<PIECES>(reg, base[0], span16[0], lane);
-      span_stage<PIECES>(span_lds, reg, span16[0], lane);
-    }
-    __syncthreads();
-    if (staged[0]) pc_tile<OUT, C>(span_lds, true, kp[0], kl[0], k0, n, seed, sink);
-    else if (t0 < ntiles) span_tile_from_hbm<OUT>(bytes, off_base, n, span_load<true>(offsets, n, t0, lane), lane, seed, sink);
-    __syncthreads();
-    __syncthreads();  // wave 1 stages
-    if (staged[1]) pc_tile<OUT, C>(span_lds, false, kp[1], kl[1], k1, n, seed, sink);
-    __syncthreads();
-  } else {
-    if (staged[1]) span_fetch<PIECES>(reg, base[1], span16[1], lane);
-    __syncthreads();
-    if (staged[0]) pc_tile<OUT, C>(span_lds, false, kp[0], kl[0], k0, n, seed, sink);
-    __syncthreads();
-    if (staged[1]) span_stage<PIECES>(span_lds, reg, span16[1], lane);
-    __syncthreads();
-    if (staged[1]) pc_tile<OUT, C>(span_lds, true, kp[1], kl[1], k1, n, seed, sink);
-    else if (t0 + 1 < ntiles)
-      span_tile_from_hbm<OUT>(bytes, off_base, n, span_load<true>(offsets, n, t0 + 1, lane), lane, seed, sink);
-    __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Paired span kernel (variable-length keys): k_span_pp's two-wave ping-pong,
-// but each wave owns a pair tile of 128 consecutive keys and each lane hashes
-// two of them back to back, paired by length (the wave's shortest key of the
-// first 64 with the longest of the second 64, and so on). A lane-per-key wave
-// runs its block loop to the tile's longest key (~31.5 of 32 blocks on U[8,512]
-// B keys whose mean is 16.25): half its VALU slots idle. Paired, a lane runs
-// to the longest pair sum (~33-34 blocks for two keys), so the same keys take
-// ~27 % fewer VALU cycles for ~9 more instructions per block (the switch from
-// the first key's chain to the second's). The pairing is a bitonic sort of the
-// 64 block counts of each half across the wave's lanes (ds_bpermute), run
-// while the span's loads are in flight.
-// The window holds a 128-key span (40 KiB: 4 workgroups = 8 waves per CU, two
-// per SIMD, so each wave may hold its 40 KiB span in 160 VGPRs while the other
-// hashes). Tiles with an invalid key or a span over the window are hashed per
-// lane straight from HBM.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kPairAlloc = 40u * 1024u;
-constexpr uint32_t kPairCap = kPairAlloc - kSpanPad;
-constexpr int kPairPieces = (kPairCap + 1023u) / 1024u;  // 40
-
-// Sort one u32 per lane across the wave, ascending (bitonic network, 21 steps).
-__device__ __forceinline__ uint32_t wave_sort_asc(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t pv = (uint32_t)__shfl_xor((int)v, (int)j);
-      const bool up = (lane & k) == 0;  // this k-block sorts ascending (k == 64: every lane)
-      const bool lower = (lane & j) == 0;
-      v = (lower == up) ? min(v, pv) : max(v, pv);
-    }
-  }
-  return v;
-}
-
-__device__ __forceinline__ void tail_lds(State& s, const uint32_t* lds, uint32_t at, uint32_t rem) {
-  if (rem) {
-    const u32x4 t = lds_read16(lds, at);
-    const uint64_t t1 = pack64(t.x, t.y) & low_bytes_mask(rem);
-    const uint64_t t2 = rem > 8 ? (pack64(t.z, t.w) & low_bytes_mask(rem - 8)) : 0ull;
-    tail_block(s, t1, t2, rem);
-  }
-}
-
-// Hash key a (la bytes at window byte pa) then key b (lb bytes at pb) in one
-// block loop: block j < nba is a's, the rest are b's; at j == nba the chain
-// state is parked in sa and restarted from the seed. Same software pipeline
-// as hash_lds_u: block j's chain beside block j+1's mixes and block j+2's read.
-__device__ __forceinline__ void hash_pair_lds(const uint32_t* lds, uint32_t pa, uint32_t la, uint32_t pb,
-                                              uint32_t lb, uint32_t seed, State& sa, State& sb) {
-  const uint32_t nba = la >> 4, nbb = lb >> 4, total = nba + nbb;
-  const uint32_t db = pb - 16u * nba;  // block j >= nba of the pair is at db + 16 j
-  State s{seed, seed};
-  sa = s;
-  const uint64_t seed64 = seed;
-  u32x4 cur = lds_read16(lds, (0u < nba ? pa : db));
-  u32x4 nxt = lds_read16(lds, (1u < nba ? pa : db) + 16u);
-  uint64_t m1 = mix_k1(pack64(cur.x, cur.y)), m2 = mix_k2(pack64(cur.z, cur.w));
-  for (uint32_t j = 0; j < total; ++j) {
-    const u32x4 nn = lds_read16(lds, (j + 2u < nba ? pa : db) + 16u * (j + 2u));
-#if SHFHB_PAIR_PREFETCH
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-    const uint64_t n1 = mix_k1(pack64(nxt.x, nxt.y)), n2 = mix_k2(pack64(nxt.z, nxt.w));
-    const bool sw = j == nba;  // first block of b: park a's chain, restart from the seed
-    sa.h1 = sw ? s.h1 : sa.h1;
-    sa.h2 = sw ? s.h2 : sa.h2;
-    s.h1 = sw ? seed64 : s.h1;
-    s.h2 = sw ? seed64 : s.h2;
-    chain_block(s, m1, m2);
-    m1 = n1;
-    m2 = n2;
-    nxt = nn;
-#if SHFHB_PAIR_PREFETCH
-    asm volatile("" : "+v"(nxt));  // block j+2's read stays a whole iteration ahead of its use
-#endif
-  }
-  if (nbb == 0) {  // b has no full block: the loop ended on a's last block
-    sa = s;
-    s = State{seed64, seed64};
-  }
-  tail_lds(sa, lds, pa + 16u * nba, la & 15u);
-  finish(sa, la);
-  tail_lds(s, lds, pb + 16u * nbb, lb & 15u);
-  finish(s, lb);
-  sb = s;
-}
-
-template <int OUT>
-__device__ __forceinline__ void hash_key_from_hbm(const uint8_t* bytes, uint64_t off_base, uint64_t key, uint64_t n,
-                                                  uint64_t o0, uint64_t o1, uint32_t seed, const Sink& sink) {
-  if (key >= n) return;
-  if (var_key_bad(o0, o1)) flag_bad_key(sink);
-  else store_result<OUT>(sink, key, hash_bytes(bytes + (o0 - off_base), (uint32_t)(o1 - o0), seed));
-}
-
-__device__ __forceinline__ uint64_t wave_read64(uint64_t v, uint32_t src_lane) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, src_lane) |
-         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), src_lane) << 32);
-}
-
-template <int OUT, int PIECES>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_span_pair(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint32_t seed, uint32_t cap, Sink sink) {
-  static_assert(OUT != kOutProbe, "probe epilogue not fused here: k_span");
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint64_t T = 2u * (uint64_t)blockIdx.x + wave;  // this wave's pair tile (past the last: idle)
-  const uint64_t k0 = T * 128u;
-  const bool has = k0 < n;
-  // lane l: key k0 + l (first half, "a") and key k0 + 64 + l (second half, "b")
-  uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-  if (has && k0 + lane < n) {
-    a0 = offsets[k0 + lane];
-    a1 = offsets[k0 + lane + 1];
-  }
-  if (has && k0 + 64u + lane < n) {
-    b0 = offsets[k0 + 64u + lane];
-    b1 = offsets[k0 + 64u + lane + 1];
-  }
-  const bool bad = __ballot(var_key_bad(a0, a1) || var_key_bad(b0, b1)) != 0;
-  const uint32_t kn = has ? (uint32_t)min<uint64_t>(128u, n - k0) : 0u;
-  // the pair tile's bytes [first, end) relative to `bytes`; offsets are monotone when no key is bad
-  const uint64_t first = wave_read64(a0, 0) - off_base;
-  const uint64_t end = (kn > 64u ? wave_read64(b1, kn - 65u) : wave_read64(a1, kn ? kn - 1u : 0u)) - off_base;
-  const uint64_t bb = reinterpret_cast<uintptr_t>(bytes);
-  const uint64_t base = (bb + first) & ~(uint64_t)15;
-  const uint64_t span = end > first ? ((bb + end + 15) & ~(uint64_t)15) - base : 0u;
-  const uint32_t span16 = span > 0xffffffffull ? 0xffffffffu : (uint32_t)span;
-  const bool staged = has && !bad && span16 <= cap;
-  u32x4 reg[PIECES];
-  if (staged && span16) span_fetch<PIECES>(reg, base, span16, lane);
-  // Pair by length while the span arrives: sort each half's block counts
-  // (low 6 bits: the key's lane), the first half ascending, the second descending.
-  const uint32_t la_own = (uint32_t)(a1 - a0), lb_own = (uint32_t)(b1 - b0);
-  // (keys past n: length 0 at window byte 0)
-  const uint32_t pa_own = k0 + lane < n ? (uint32_t)(bb + (a0 - off_base) - base) : 0u;
-  const uint32_t pb_own = k0 + 64u + lane < n ? (uint32_t)(bb + (b0 - off_base) - base) : 0u;
-  uint32_t pa = 0, la = 0, pb = 0, lb = 0, ia = 0, ib = 0;
-  if (staged) {
-    const uint32_t ka = wave_sort_asc((min(la_own >> 4, 0x3ffffffu) << 6) | lane, lane);
-    const uint32_t kb = ~wave_sort_asc(~((min(lb_own >> 4, 0x3ffffffu) << 6) | lane), lane);
-    ia = ka & 63u;
-    ib = kb & 63u;
-    pa = (uint32_t)__shfl((int)pa_own, (int)ia);
-    la = (uint32_t)__shfl((int)la_own, (int)ia);
-    pb = (uint32_t)__shfl((int)pb_own, (int)ib);
-    lb = (uint32_t)__shfl((int)lb_own, (int)ib);
-  }
-#pragma unroll
-  for (uint32_t phase = 0; phase < 2; ++phase) {
-    if (wave == phase && staged && span16) span_stage<PIECES>(span_lds, reg, span16, lane);
-    __syncthreads();
-    if (wave == phase && has) {
-      if (staged) {
-        State sa, sb;
-        hash_pair_lds(span_lds, pa, la, pb, lb, seed, sa, sb);
-        if (k0 + ia < n) store_result<OUT>(sink, k0 + ia, sa);
-        if (k0 + 64u + ib < n) store_result<OUT>(sink, k0 + 64u + ib, sb);
-      } else {
-        hash_key_from_hbm<OUT>(bytes, off_base, k0 + lane, n, a0, a1, seed, sink);
-        hash_key_from_hbm<OUT>(bytes, off_base, k0 + 64u + lane, n, b0, b1, seed, sink);
       }
     }
     __syncthreads();
@@ -1500,43 +1072,6 @@ static hipError_t launch_span_p(const void* bytes, const uint64_t* offsets, uint
 // at 10 vs 20 KiB, profiles/r1/ab_window/, ab_sized/).
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
-// Producer/consumer span kernel: one 128-thread workgroup per two tiles, one window.
-template <int OUT>
-static hipError_t launch_var_span_pc(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                                     uint32_t seed, const Sink& sink, hipStream_t st) {
-  const uint64_t tiles = (n + 63) / 64;
-  const uint64_t wgs = (tiles + 1) / 2;
-  if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_span_pc<OUT, kSpanPiecesMax>), dim3((unsigned)wgs), dim3(128), kSpanAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
-  return hipGetLastError();
-}
-
-// Persistent ping-pong span kernel: a resident grid of two-wave workgroups.
-template <int OUT>
-static hipError_t launch_var_span_persist(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                                          uint32_t seed, const Sink& sink, hipStream_t st) {
-  const uint64_t tiles = (n + 63) / 64;
-  const unsigned res = resident_grid(reinterpret_cast<const void*>(&k_span_pq<OUT, kSpanPiecesMax>), 128, kSpanAlloc,
-                                     20 + OUT);
-  const unsigned g = grid_for((tiles + 1) / 2, 1, res * SHFHB_PQ_GRID_MULT);
-  hipLaunchKernelGGL((k_span_pq<OUT, kSpanPiecesMax>), dim3(g), dim3(128), kSpanAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
-  return hipGetLastError();
-}
-
-// Paired span kernel: one 128-thread workgroup per two 128-key pair tiles.
-template <int OUT>
-static hipError_t launch_var_span_pair(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                                       uint32_t seed, const Sink& sink, hipStream_t st) {
-  const uint64_t ptiles = (n + 127) / 128;
-  const uint64_t wgs = (ptiles + 1) / 2;
-  if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_span_pair<OUT, kPairPieces>), dim3((unsigned)wgs), dim3(128), kPairAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kPairCap, sink);
-  return hipGetLastError();
-}
-
 // Ping-pong span kernel: one 128-thread workgroup per two tiles, one window.
 template <int OUT>
 static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
@@ -1575,17 +1110,9 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
   if constexpr (VAR) {
     const double need = key_bytes && n ? 64.0 * (double)key_bytes / (double)n * 1.1 + 512.0 + kSpanPad : 1e30;
     // windows over 10 KiB (config D's U[8,512] B keys): two waves per window
-    if constexpr (OUT != kOutProbe) {
-      // pair tiles whose expected span fits the 40-KiB window: two keys per lane
-      if (SHFHB_SPAN_PAIR && need > 10240.0 + kSpanPad && 2.0 * (need - 512.0 - kSpanPad) + 512.0 <= kPairCap)
-        return launch_var_span_pair<OUT>(bytes, offsets, off_base, n, seed, sink, st);
-      if (SHFHB_SPAN_PC && need > 10240.0 + kSpanPad)
-        return launch_var_span_pc<OUT>(bytes, offsets, off_base, n, seed, sink, st);
-      if (SHFHB_SPAN_PQ && need > 10240.0 + kSpanPad)
-        return launch_var_span_persist<OUT>(bytes, offsets, off_base, n, seed, sink, st);
+    if constexpr (OUT != kOutProbe)
       if (SHFHB_SPAN_PINGPONG && need > 10240.0 + kSpanPad)
         return launch_var_span_pingpong<OUT>(bytes, offsets, off_base, n, seed, sink, st);
-    }
     if (need >= (double)kSpanAlloc)
       return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, kSpanAlloc);
     const uint32_t w = (uint32_t)need;
