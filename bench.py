@@ -61,7 +61,12 @@ BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for 
 
 # rocprofv3 kernel-name substrings of each workload's kernel (PMC passes)
 KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
-               "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>"}
+               "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>",
+               "tabpart": "k_tab_split"}
+# kernels whose reads are not 16-B-per-lane streams: FETCH_SIZE's x2 (calibrated for those only,
+# MI355X_MICROARCH.md "HBM") is not known to hold, so their traffic is reported raw beside it
+FETCH_UNCALIBRATED = {"probe16": "128-B row gathers (8 lanes x 16 B) and 4-B tab-map lookups",
+                      "tabpart": "8-B ref loads and byte/dword record gathers"}
 
 
 def parse(argv=None):
@@ -76,8 +81,9 @@ def parse(argv=None):
                    help="configs[4]: 16-B keys for the whole job, split over the GPUs (strong scaling)")
     p.add_argument("--keys256", type=int, default=100_000_000, help="configs[2]: 256-B keys per GPU")
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
-    p.add_argument("--only", default="", help="comma list of fixed16,fixed16_hot,shard1b,fixed256,var,probe16")
+    p.add_argument("--only", default="", help="comma list of fixed16,fixed16_hot,shard1b,fixed256,var,probe16,tabpart")
     p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
+    p.add_argument("--tab-jobs", type=int, default=1024, help="tabpart: tabs parted per step (f4)")
     p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -253,7 +259,7 @@ def make_workloads(args, dev, rank, world=1):
     from sharedhashfile_amd.keygen import device_random_bytes
 
     only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed16_hot", "shard1b", "fixed256", "var",
-                                                        "probe16"}
+                                                        "probe16", "tabpart"}
     wl = []
     seed_base = 0x5348460000000001 + 1000 * rank
     fk16 = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
@@ -351,8 +357,90 @@ def make_workloads(args, dev, rank, world=1):
                      "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed), verify_probe)
         w.index = index
         wl.append(w)
+    if "tabpart" in only:
+        wl.append(tab_workload(args, dev, seed_base))
     torch.cuda.synchronize()
     return wl
+
+
+def tab_workload(args, dev, seed_base):
+    """f4: shf_tab_part()'s copy of a batch of full tabs,
+    one job per tab (shf.c:722-779 + the shrink :678-720), device-resident.
+    Synthetic tabs at part time (sharedhashfile_amd/tabgen.py: 4500 refs,
+    keys U[16,64] B, values U[8,128] B, ~0.5 MB of records each), every job
+    its own copy in HBM so that nothing is re-read from cache."""
+    import ctypes
+
+    import torch
+
+    import sharedhashfile_amd as hb
+    from sharedhashfile_amd.tabgen import algorithmic_bytes, synth_tab
+
+    nb = 8
+    base = [synth_tab(seed_base + 50 + i) for i in range(nb)]
+    maps, news = [], []
+    for _, m, old in base:
+        new = (old + 1000) % 2048
+        maps.append(hb.tab_part_redirect(m, old, new))
+        news.append(new)
+    al = lambda x: (x + 4095) // 4096 * 4096
+    J = args.tab_jobs
+    sizes = [al(img.size) for img, _, _ in base]
+    jobs = (hb.TabJob * J)()
+    soff = doff = 0
+    for j in range(J):
+        b = j % nb
+        jb = jobs[j]
+        jb.src, jb.src_len, jb.cap, jb.map, jb.tab_new = soff, base[b][0].size, sizes[b], b, news[b]
+        jb.keep, jb.move = doff, doff + sizes[b]
+        jb.keep_type, jb.move_type = 0x3E, 0x3E
+        soff += sizes[b]
+        doff += 2 * sizes[b]
+    src = torch.zeros(soff, dtype=torch.uint8, device=dev)
+    for b, (img, _, _) in enumerate(base):
+        t = torch.from_numpy(img).to(dev)
+        for j in range(b, J, nb):
+            src[jobs[j].src:jobs[j].src + img.size].copy_(t)
+    dst = torch.zeros(doff, dtype=torch.uint8, device=dev)
+    d_jobs = torch.from_numpy(np.frombuffer(bytes(jobs), dtype=np.uint8).copy()).to(dev)
+    d_maps = torch.from_numpy(np.stack(maps).view(np.int16)).to(dev)
+    prm = hb.TabParams(0, 0, 0, 1)
+    fn = hb.load().shf_tab_copy_batch_async
+    argv = (ctypes.c_void_p(src.data_ptr()), ctypes.c_uint64(soff), ctypes.c_void_p(dst.data_ptr()),
+            ctypes.c_uint64(doff), ctypes.c_void_p(d_jobs.data_ptr()), ctypes.c_uint32(J),
+            ctypes.c_void_p(d_maps.data_ptr()), ctypes.c_uint32(nb), ctypes.byref(prm),
+            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+
+    def launch():
+        rc = fn(*argv)
+        if rc:
+            raise hb.ShfHashBatchError(rc, "shf_tab_copy_batch_async")
+
+    def verify():
+        from oracle.oracle_py import Oracle
+
+        o = Oracle()
+        done = (hb.TabJob * J).from_buffer_copy(d_jobs.cpu().numpy().tobytes())
+        if any(done[j].status != hb.OK for j in range(J)):
+            return False, 0
+        ok, checked = True, 0
+        for j in sorted({0, J - 1, J // 3, (2 * J) // 3} | set(range(min(nb, J)))):
+            b = j % nb
+            keep = dst[jobs[j].keep:jobs[j].keep + sizes[b]].cpu().numpy()
+            move = dst[jobs[j].move:jobs[j].move + sizes[b]].cpu().numpy()
+            wk, wm = o.tab_split(base[b][0], maps[b], news[b], cap=sizes[b], keep_type=0x3E, move_type=0x3E)
+            ok = ok and np.array_equal(keep, wk) and np.array_equal(move, wm)
+            checked += 1
+        return bool(ok), checked
+
+    per_job = float(np.mean([algorithmic_bytes(base[j % nb][0]) for j in range(J)]))
+    w = Workload("tabpart", J, per_job, [launch], "k_tab_split",
+                 "%d tab parts per step (f4: shf_tab_part's copy, both output tabs), synthetic tabs of 4500 refs "
+                 "with %.2f MB of records each, %.2f GB moved per step" % (
+                     J, float(np.mean([img.size - 65560 for img, _, _ in base])) / 1e6, J * per_job / 1e9), verify)
+    w.unit = "tabs/s"
+    w.keep = (src, dst, d_jobs, d_maps, prm)
+    return w
 
 
 def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP_MIN_S):
@@ -732,10 +820,14 @@ def run_rank(args):
             c = (pmc or {}).get(name if name not in ("fixed16_hot", "shard1b") else "fixed16")
             if c:
                 # keys per launch in the PMC child (configs 2/3 run there at <= 10M keys)
-                pk = {"fixed256": min(args.keys256, 10_000_000), "var": min(args.keysvar, 10_000_000)}.get(
-                    name, args.keys16)
+                pk = {"fixed256": min(args.keys256, 10_000_000), "var": min(args.keysvar, 10_000_000),
+                      "tabpart": args.tab_jobs}.get(name, args.keys16)
                 f = pmc_fields(c, pk * r["bytes_per_key"])
-                if name in ("fixed16", "fixed16_hot", "probe16"):
+                if name in FETCH_UNCALIBRATED:
+                    ro["fetch_size_raw"] = c.get("FETCH_SIZE", 0) * 1024.0
+                    ro["write_size"] = c.get("WRITE_SIZE", 0) * 1024.0
+                    ro["fetch_x2_uncalibrated"] = FETCH_UNCALIBRATED[name]
+                if name in ("fixed16", "fixed16_hot", "probe16", "tabpart"):
                     ro["traffic"] = f.get("traffic")
                 else:
                     ro["traffic_at_pmc_size"] = f.get("traffic")
@@ -749,11 +841,13 @@ def run_rank(args):
             else None
         roof["traffic_note"] = pmc_note
         secondary = {}
+        wmap = {w.name: w for w in wl}
         for name, r in results.items():
             if name == head_name:
                 continue
             secondary[name] = {"value": r["value"], "value_min": r["value_min"], "value_max": r["value_max"],
-                               "unit": "keys/s", "ms_per_step": round(r["ms_per_step"], 4), "desc": r["desc"],
+                               "unit": getattr(wmap[name], "unit", "keys/s"), "ms_per_step": round(r["ms_per_step"], 4),
+                               "desc": r["desc"],
                                "roofline": roofline(name, r), "verified": verified.get(name)}
             if name == "shard1b":
                 secondary[name]["scaling"] = "strong"

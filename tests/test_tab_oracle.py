@@ -79,3 +79,30 @@ def test_oracle_part_matches_live_reference(oracle, lo, hi, fk, fv, fac):
     for cap in caps:
         _, (keep, move) = oracle_part(oracle, cap)
         tabcheck.check_capture(cap, keep, move, int(off[cap["key"] + 1] - off[cap["key"]]))
+
+
+def test_synthetic_bench_tabs_split_cleanly(oracle):
+    """The bench's synthetic tabs (sharedhashfile_amd/tabgen.py) are tabs the
+    oracle parts: every used ref lands in exactly one output with its record
+    intact, the keep and move records add up to the source's data."""
+    from sharedhashfile_amd.tabgen import TAB_DATA, TAB_HDR, algorithmic_bytes, synth_tab
+
+    img, m, old = synth_tab(3, n_refs=2000)
+    new = (old + 1000) % 2048
+    m2 = oracle.tab_part_redirect(m, old, new)
+    keep, move = oracle.tab_split(img, m2, new, cap=img.size)
+    hs, hk, hm = (tabcheck.hdr(x) for x in (img, keep, move))
+    assert hk[5] + hm[5] == hs[5] and hk[2] // 2 + hm[2] // 2 == 2000
+    assert 0 < hm[2] < hk[2] + hm[2]  # both outputs get refs
+    rs, rk, rm = (x[TAB_HDR:TAB_DATA].view(np.uint32).reshape(-1, 2) for x in (img, keep, move))
+    used = rs[:, 1] != 0
+    assert np.array_equal(used, (rk[:, 1] != 0) | (rm[:, 1] != 0)) and not ((rk[:, 1] != 0) & (rm[:, 1] != 0)).any()
+    for i in np.nonzero(used)[0][:200]:
+        out, r = (keep, rk) if rk[i, 1] else (move, rm)
+        kl = int(img[rs[i, 1] + 1:rs[i, 1] + 5].view(np.uint32)[0])
+        vl = int(img[rs[i, 1] + 5 + kl:rs[i, 1] + 9 + kl].view(np.uint32)[0])
+        n = 9 + kl + vl
+        # byte 0 is the copy's data-type byte (0x3e / 0xbe, oracle/tab_oracle.h)
+        assert out[r[i, 1]] in (0x3E, 0xBE)
+        assert np.array_equal(out[r[i, 1] + 1:r[i, 1] + n], img[rs[i, 1] + 1:rs[i, 1] + n])
+    assert algorithmic_bytes(img) == 3 * TAB_DATA + 2 * hs[5]

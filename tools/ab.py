@@ -40,7 +40,7 @@ def build(name, flags, outdir):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--variant", action="append", required=True, help="name=-Dflags ...")
-    p.add_argument("--workload", default="fixed256", choices=["fixed16", "fixed256", "var", "fixedL", "probe16", "probeh"])
+    p.add_argument("--workload", default="fixed256", choices=["fixed16", "fixed256", "var", "fixedL", "probe16", "probeh", "tab"])
     p.add_argument("--key-len", type=int, default=37)
     p.add_argument("--n", type=int, default=20_000_000)
     p.add_argument("--rounds", type=int, default=6)
@@ -94,6 +94,22 @@ def main():
             per_key = 16 + 128 + 16
             call = lambda lib, out: lib.shf_probe_batch_hashes_async(index.handle, h.data_ptr(), n, out.data_ptr(),
                                                                      None)
+    elif a.workload == "tab":  # f4: the bench's tab-part batch (bench.py tab_workload), a.n tabs
+        import bench
+
+        class _A:
+            tab_jobs = a.n
+
+        tw = bench.tab_workload(_A, dev, 0x5348460000000001)
+        src, dst, d_jobs, d_maps, prm = tw.keep
+        per_key = tw.bytes_per_key
+        out_shape = None
+
+        def call(lib, out):
+            return lib.shf_tab_copy_batch_async(ctypes.c_void_p(src.data_ptr()), src.numel(),
+                                                ctypes.c_void_p(out.data_ptr()), out.numel(),
+                                                ctypes.c_void_p(d_jobs.data_ptr()), n, ctypes.c_void_p(d_maps.data_ptr()),
+                                                8, ctypes.byref(prm), cs())
     elif a.workload in ("fixed16", "fixed256", "fixedL"):
         L = {"fixed16": 16, "fixed256": 256, "fixedL": a.key_len}[a.workload]
         keys = device_random_bytes(n * L, 1, dev)
@@ -115,8 +131,11 @@ def main():
         else:
             call = lambda lib, out: lib.shf_hash_batch_var_kernel_async(data.data_ptr(), off.data_ptr(), n, 12345,
                                                                          out.data_ptr(), a.kernel, cs())
-    outs = {k: torch.empty(out_shape, dtype=torch.int64 if out_shape[1] == 2 else torch.int32, device=dev)
-            for k in libs}
+    if out_shape is None:  # tab: each variant writes its own copy of the output images
+        outs = {k: torch.zeros_like(dst) for k in libs}
+    else:
+        outs = {k: torch.empty(out_shape, dtype=torch.int64 if out_shape[1] == 2 else torch.int32, device=dev)
+                for k in libs}
     for k, lib in libs.items():
         assert call(lib, outs[k]) == 0
     torch.cuda.synchronize()
