@@ -40,7 +40,6 @@ constexpr uint32_t kTabData = kTabHdr + kTabRefs * 8;     // offsetof(SHF_TAB_MM
 constexpr uint32_t kPage = 4096;                          // SHF_SIZE_PAGE
 constexpr uint32_t kThreads = 512;
 constexpr uint32_t kWaves = kThreads / 64;
-constexpr uint32_t kRefsPerThread = kTabRefs / kThreads;  // 16: one row
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
@@ -88,6 +87,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
+// One image's records in image order, in LDS: rank r at e[base + dir * r] (the
+// keep image's list grows up from 0, the move image's down from the top, so
+// the two never meet: a tab has at most 8192 records). end(r) = the record's
+// end in the image's data, pos(r) = its byte in the source image.
+struct RecList {
+  const uint32_t* e_end;
+  const uint32_t* e_pos;
+  int32_t base, dir;
+  __device__ uint32_t end(uint32_t r) const { return e_end[base + dir * (int32_t)r]; }
+  __device__ uint32_t pos(uint32_t r) const { return e_pos[base + dir * (int32_t)r]; }
+};
+
 // tab_size after appending an image's records in order to a fresh tab
 // (SHF_GET_TAB_MMAP's initial size MOD_PAGE(sizeof(SHF_TAB_MMAP)), then
 // SHF_TAB_APPEND's growth MOD_PAGE(tab_size + data_needed * factor) whenever a
@@ -95,20 +106,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 // the image's records (increasing). One wave; every lane returns the size.
 // The first record whose end exceeds the room is found 64 ends at a time,
 // moving forward only.
-__device__ uint64_t replay_tab_size(const uint32_t* ends, uint32_t n, uint32_t factor, uint32_t lane) {
+__device__ uint64_t replay_tab_size(const RecList& L, uint32_t n, uint32_t factor, uint32_t lane) {
   uint64_t size = mod_page(kTabData);
   uint32_t i0 = 0;
   for (;;) {
     const uint64_t room = size - kTabData;
     uint64_t hit = 0;
     while (i0 < n) {
-      hit = __ballot(i0 + lane < n && (uint64_t)ends[i0 + lane] > room);
+      hit = __ballot(i0 + lane < n && (uint64_t)L.end(i0 + lane) > room);
       if (hit) break;
       i0 += 64;
     }
     if (!hit) return size;
     i0 += (uint32_t)__builtin_ctzll(hit);  // first record that does not fit
-    const uint32_t len = ends[i0] - (i0 ? ends[i0 - 1] : 0u);
+    const uint32_t len = L.end(i0) - (i0 ? L.end(i0 - 1) : 0u);
     size = mod_page(size + (uint64_t)len * factor);
   }
 }
@@ -134,17 +145,92 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
   *reinterpret_cast<volatile int32_t*>(&job->status) = v;
 }
 
+#ifndef SHFHB_TAB_CHUNKS
+#define SHFHB_TAB_CHUNKS 2  // 16-B chunks per lane in flight (2 and 4 within 5 %, 8 slower: profiles/r2/ab_tab)
+#endif
+
+// Copy the image's data chunks [c_begin, c_end) (absolute 16-B chunks; the
+// image's data starts at absolute byte d0 and its records [0, nrec) are in L,
+// `total` bytes of them): consecutive chunks on consecutive lanes of the
+// workgroup, SHFHB_TAB_CHUNKS per lane in flight. A chunk takes its bytes from
+// the record holding its first byte (binary search of the ends) and the next
+// ones where it crosses a record end; a record's first byte is its
+// SHF_DATA_TYPE, written as the job says (shf.c:593-596). Only the data's
+// bytes are written (a chunk straddling its start or end is stored partially).
+__device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList& L, uint32_t nrec, uint64_t total,
+                            uint64_t d0, uint64_t c_begin, uint64_t c_end, uint32_t type, uint32_t t) {
+  constexpr uint32_t Q = SHFHB_TAB_CHUNKS;
+  for (uint64_t base = c_begin; base < c_end; base += Q * kThreads) {
+    unsigned __int128 v[Q];
+    uint32_t k[Q], lo[Q], hi[Q], st[Q];
+    int64_t a[Q];
+#pragma unroll
+    for (uint32_t q = 0; q < Q; ++q) {
+      const uint64_t c = base + q * kThreads + t;
+      a[q] = (int64_t)(c << 4) - (int64_t)d0;  // the chunk's first byte in the image's data
+      lo[q] = a[q] < 0 ? 0u : (uint32_t)a[q];
+      hi[q] = c < c_end ? (uint32_t)min<int64_t>(a[q] + 16, (int64_t)total) : lo[q];
+      uint32_t l = 0, h = nrec;  // first record ending past lo
+      while (l < h) {
+        const uint32_t mid = (l + h) >> 1;
+        if (L.end(mid) > lo[q]) h = mid;
+        else l = mid + 1;
+      }
+      k[q] = l;
+      if (lo[q] < hi[q]) {
+        st[q] = l ? L.end(l - 1) : 0u;
+        v[q] = load16(src, src_len, (uint64_t)L.pos(l) + (lo[q] - st[q]));
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < Q; ++q) {
+      if (lo[q] >= hi[q]) continue;
+      unsigned __int128 out = 0, x = v[q];
+      uint32_t b = lo[q], s0 = st[q], kk = k[q];
+      for (;;) {
+        const uint32_t e = L.end(kk), take = min(e, hi[q]) - b, o = (uint32_t)((int64_t)b - a[q]);
+        if (b == s0) x = (x & ~(unsigned __int128)0xff) | type;
+        out |= (x & low_bytes128(take)) << (8 * o);
+        b += take;
+        if (b >= hi[q]) break;
+        s0 = e;
+        ++kk;
+        x = load16(src, src_len, L.pos(kk));
+      }
+      uint8_t* dst = reinterpret_cast<uint8_t*>((base + q * kThreads + t) << 4);
+      const uint32_t o = (uint32_t)((int64_t)lo[q] - a[q]);  // the chunk's first byte it writes
+      const uint32_t n = hi[q] - lo[q];
+      if (n == 16u) {
+        *reinterpret_cast<u32x4*>(dst) =
+            u32x4{(uint32_t)out, (uint32_t)(out >> 32), (uint32_t)(out >> 64), (uint32_t)(out >> 96)};
+      } else {
+        const unsigned __int128 y = out >> (8 * o);
+        store_partial(dst + o, u32x4{(uint32_t)y, (uint32_t)(y >> 32), (uint32_t)(y >> 64), (uint32_t)(y >> 96)}, n);
+      }
+    }
+  }
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(kThreads) void k_tab_split(const uint8_t* __restrict__ src_base, uint64_t src_bytes,
+// Segments of refs processed in order: each reads its refs' length words and
+// copies its records while the lines those reads pulled in are still in L2 /
+// the Infinity Cache (one pass over the whole tab's lengths first would evict
+// them before the copy at 2 tabs per CU: the data are read twice from HBM).
+#ifndef SHFHB_TAB_SEGS
+#define SHFHB_TAB_SEGS 4
+#endif
+constexpr uint32_t kSegs = SHFHB_TAB_SEGS;
+constexpr uint32_t kSegRefs = kTabRefs / kSegs;           // 2048
+constexpr uint32_t kSlabs = kSegRefs / kThreads;          // 4: ref = seg * 2048 + slab * 512 + thread
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_tab_split(const uint8_t* __restrict__ src_base, uint64_t src_bytes,
                                                         uint8_t* dst_base, uint64_t dst_bytes, shf_tab_job* jobs,
                                                         const uint16_t* __restrict__ maps, uint32_t n_maps,
                                                         shf_tab_params prm) {
-  // the records of both images in image order: keep's at [0, refs_keep), move's after them;
-  // e_end = the record's end in its image's data (inclusive scan of the sizes), e_pos = its source byte
-  __shared__ uint32_t e_end[kTabRefs];
+  __shared__ uint32_t e_end[kTabRefs];  // both images' record lists (RecList)
   __shared__ uint32_t e_pos[kTabRefs];
-  __shared__ uint32_t wsum[4][kWaves];     // per wave: keep bytes, move bytes, keep refs, move refs
+  __shared__ uint32_t wsum[2][kSlabs][4][kWaves];  // per segment parity, slab, quantity (keep/move bytes/refs), wave
   __shared__ int bad;
   shf_tab_job* job = jobs + blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
@@ -154,9 +240,10 @@ __global__ __launch_bounds__(kThreads) void k_tab_split(const uint8_t* __restric
   const uint16_t* map = moving ? maps + (uint64_t)job->map * 2048u : maps;
   const uint32_t len_len = prm.fixed ? 0u : 4u;  // shf.c:674
   const uint32_t factor = prm.data_needed_factor ? prm.data_needed_factor : 1u;
+  const uint32_t tab_new = job->tab_new, keep_type = job->keep_type, move_type = job->move_type;
+  const uint64_t cap = job->cap;
   if (t == 0) {
     // every byte a job names lies in its buffer; images are 8-B aligned
-    const uint64_t cap = job->cap;
     bad = src_len < kTabData || job->src > src_bytes || src_len > src_bytes - job->src || cap < kTabData ||
           job->keep > dst_bytes || cap > dst_bytes - job->keep ||
           (moving && (job->move > dst_bytes || cap > dst_bytes - job->move || job->map >= n_maps)) ||
@@ -167,217 +254,148 @@ __global__ __launch_bounds__(kThreads) void k_tab_split(const uint8_t* __restric
     if (t == 0) flag(job, SHF_HB_ERR_ARG);
     return;
   }
+  uint8_t* keep = dst_base + job->keep;
+  uint8_t* move = moving ? dst_base + job->move : nullptr;
+  const RecList LK{e_end, e_pos, 0, 1}, LM{e_end, e_pos, (int32_t)kTabRefs - 1, -1};
+  const uint64_t d0k = reinterpret_cast<uintptr_t>(keep + kTabData), d0m = reinterpret_cast<uintptr_t>(move + kTabData);
+  // what the segments before this one hold (workgroup-uniform)
+  uint64_t done_keep = 0, done_move = 0;   // data bytes
+  uint32_t refs_keep = 0, refs_move = 0;   // records
+  uint64_t next_k = d0k >> 4, next_m = d0m >> 4;  // the first chunk not yet copied
 
-  // 1. this thread's row: refs {tab:11 | rnd:21, pos} (shf.private.h:48-52), record lengths
-  uint32_t w0[kRefsPerThread], pos[kRefsPerThread], len[kRefsPerThread];
-  const u32x4* row = reinterpret_cast<const u32x4*>(src + kTabHdr + (uint64_t)t * kRefsPerThread * 8u);
+  for (uint32_t seg = 0; seg < kSegs; ++seg) {
+    // 1. this thread's refs {tab:11 | rnd:21, pos} (shf.private.h:48-52) and their record lengths
+    uint32_t w0[kSlabs], pos[kSlabs], len[kSlabs], kl[kSlabs];
+    bool mine_bad = false;
 #pragma unroll
-  for (uint32_t q = 0; q < kRefsPerThread / 2; ++q) {  // 8-B aligned: two 8-B loads' worth as one 16-B load
-    const u32x4 r = *reinterpret_cast<const u32x4_a1*>(row + q);
-    w0[2 * q] = r.x;
-    pos[2 * q] = r.y;
-    w0[2 * q + 1] = r.z;
-    pos[2 * q + 1] = r.w;
-  }
-  // SHF_TAB_REF_COPY's lengths (shf.c:636-637): the key length word, then the value length word after the key
-  bool mine_bad = false;
-  uint32_t kl[kRefsPerThread];
-#pragma unroll
-  for (uint32_t j = 0; j < kRefsPerThread; ++j) {
-    kl[j] = prm.fixed_key_len;
-    if (!prm.fixed && pos[j] != 0) {
-      if (pos[j] < kTabData || (uint64_t)pos[j] + 9u > src_len) mine_bad = true;
-      else kl[j] = load_u32(src + pos[j] + 1);
+    for (uint32_t j = 0; j < kSlabs; ++j) {
+      const uint32_t r = seg * kSegRefs + j * kThreads + t;
+      const uint2 ref = *reinterpret_cast<const uint2*>(src + kTabHdr + 8u * r);  // 8-B aligned
+      w0[j] = ref.x;
+      pos[j] = ref.y;
     }
-  }
-  uint32_t to_move = 0;  // bit j: ref j goes to the move image
-  uint32_t sum_keep = 0, sum_move = 0, n_keep = 0, n_move = 0;
+    // SHF_TAB_REF_COPY's lengths (shf.c:636-637): the key length word, then the value length word after the key
 #pragma unroll
-  for (uint32_t j = 0; j < kRefsPerThread; ++j) {
-    len[j] = 0;
-    if (pos[j] == 0) continue;  // ref unused
-    const uint64_t p = pos[j];
-    uint32_t vl = prm.fixed_val_len;
-    if (!prm.fixed) {
-      if (p < kTabData || p + 9u + kl[j] > src_len) {
+    for (uint32_t j = 0; j < kSlabs; ++j) {
+      kl[j] = prm.fixed_key_len;
+      if (!prm.fixed && pos[j] != 0) {
+        if (pos[j] < kTabData || (uint64_t)pos[j] + 9u > src_len) mine_bad = true;
+        else kl[j] = load_u32(src + pos[j] + 1);
+      }
+    }
+    uint32_t to_move = 0;  // bit j: ref of slab j goes to the move image
+#pragma unroll
+    for (uint32_t j = 0; j < kSlabs; ++j) {
+      len[j] = 0;
+      if (pos[j] == 0) continue;  // ref unused
+      const uint64_t p = pos[j];
+      uint32_t vl = prm.fixed_val_len;
+      if (!prm.fixed) {
+        if (p < kTabData || p + 9u + kl[j] > src_len) {
+          mine_bad = true;
+          continue;
+        }
+        vl = load_u32(src + p + 5 + kl[j]);
+      }
+      const uint64_t l = 1ull + len_len + kl[j] + len_len + vl;
+      if (p < kTabData || p + l > src_len || l > 0xffffffffull) {
         mine_bad = true;
         continue;
       }
-      vl = load_u32(src + p + 5 + kl[j]);
+      len[j] = (uint32_t)l;
+      to_move |= (uint32_t)(moving && map[w0[j] & 0x7ffu] == tab_new) << j;  // shf.c:765-767
     }
-    const uint64_t l = 1ull + len_len + kl[j] + len_len + vl;
-    if (p < kTabData || p + l > src_len || l > 0xffffffffull) {
-      mine_bad = true;
-      continue;
-    }
-    len[j] = (uint32_t)l;
-    const bool mv = moving && map[w0[j] & 0x7ffu] == job->tab_new;  // shf.c:765-767
-    to_move |= (uint32_t)mv << j;
-    if (mv) {
-      sum_move += (uint32_t)l;
-      ++n_move;
-    } else {
-      sum_keep += (uint32_t)l;
-      ++n_keep;
-    }
-  }
-  if (mine_bad) bad = 1;
+    if (mine_bad) bad = 1;
 
-  // 2. exclusive scans of the per-thread sums: in the wave, then over the waves
-  const uint32_t ik = wave_incl_scan(sum_keep, lane), im = wave_incl_scan(sum_move, lane);
-  const uint32_t ck = wave_incl_scan(n_keep, lane), cm = wave_incl_scan(n_move, lane);
-  if (lane == 63) {
-    wsum[0][wave] = ik;
-    wsum[1][wave] = im;
-    wsum[2][wave] = ck;
-    wsum[3][wave] = cm;
-  }
-  __syncthreads();
-  uint64_t total_keep = 0, total_move = 0;
-  uint32_t base_keep = 0, base_move = 0, refs_keep = 0, refs_move = 0;
+    // 2. scans in ref order (slab by slab, thread by thread): in the wave, then over the waves
+    //    through LDS. Per ref: its size in keep, in move, and the keep and move record counts
+    //    packed in one word. The in-wave scans are recomputed after the barrier rather than held.
 #pragma unroll
-  for (uint32_t w = 0; w < kWaves; ++w) {
-    total_keep += wsum[0][w];
-    total_move += wsum[1][w];
-    refs_keep += wsum[2][w];
-    refs_move += wsum[3][w];
-    if (w < wave) {
-      base_keep += wsum[0][w];
-      base_move += wsum[1][w];
+    for (uint32_t j = 0; j < kSlabs; ++j) {
+      const bool mv = (to_move >> j) & 1u;
+      const uint32_t ik = wave_incl_scan(mv ? 0u : len[j], lane), im = wave_incl_scan(mv ? len[j] : 0u, lane);
+      const uint32_t ic = wave_incl_scan(len[j] ? (mv ? 0x10000u : 1u) : 0u, lane);
+      if (lane == 63) {
+        wsum[seg & 1][j][0][wave] = ik;
+        wsum[seg & 1][j][1][wave] = im;
+        wsum[seg & 1][j][2][wave] = ic;
+      }
+    }
+    __syncthreads();
+    uint64_t seg_k = 0, seg_m = 0;  // this segment's keep and move bytes so far
+    uint32_t seg_c = 0;             // and records (packed: keep low, move high half)
+    // 3. each ref's record offset in its image, its list entry, its row entry in both images
+#pragma unroll
+    for (uint32_t j = 0; j < kSlabs; ++j) {
+      const bool mv = (to_move >> j) & 1u, used = len[j] != 0;
+      const uint32_t ik = wave_incl_scan(mv ? 0u : len[j], lane), im = wave_incl_scan(mv ? len[j] : 0u, lane);
+      const uint32_t ic = wave_incl_scan(used ? (mv ? 0x10000u : 1u) : 0u, lane);
+      uint32_t bk = 0, bm = 0, bc = 0, ak = 0, am = 0, ac = 0;  // before this wave / whole slab
+#pragma unroll
+      for (uint32_t w = 0; w < kWaves; ++w) {
+        const uint32_t vk = wsum[seg & 1][j][0][w], vm = wsum[seg & 1][j][1][w], vc = wsum[seg & 1][j][2][w];
+        ak += vk;
+        am += vm;
+        ac += vc;
+        if (w < wave) {
+          bk += vk;
+          bm += vm;
+          bc += vc;
+        }
+      }
+      const uint32_t r = seg * kSegRefs + j * kThreads + t;
+      const uint32_t end = mv ? (uint32_t)(done_move + seg_m) + bm + im : (uint32_t)(done_keep + seg_k) + bk + ik;
+      const uint32_t at = kTabData + end - len[j];  // inclusive end - size = this record's offset
+      if (used) {
+        const uint32_t c = seg_c + bc + ic;  // inclusive counts in this segment
+        const uint32_t rank = mv ? refs_move + (c >> 16) - 1u : refs_keep + (c & 0xffffu) - 1u;
+        const uint32_t i = mv ? kTabRefs - 1u - rank : rank;
+        e_end[i] = end;
+        e_pos[i] = pos[j];
+      }
+      *reinterpret_cast<uint2*>(keep + kTabHdr + 8u * r) = (used && !mv) ? make_uint2(w0[j], at) : make_uint2(0u, 0u);
+      if (moving)
+        *reinterpret_cast<uint2*>(move + kTabHdr + 8u * r) = (used && mv) ? make_uint2(w0[j], at) : make_uint2(0u, 0u);
+      seg_k += ak;
+      seg_m += am;
+      seg_c += ac;
+    }
+    const uint64_t seg_tot[4] = {seg_k, seg_m, seg_c & 0xffffu, seg_c >> 16};
+    done_keep += seg_tot[0];
+    done_move += seg_tot[1];
+    refs_keep += (uint32_t)seg_tot[2];
+    refs_move += (uint32_t)seg_tot[3];
+    if (t == 0 && (kTabData + done_keep > cap || (moving && kTabData + done_move > cap) ||
+                   kTabData + done_keep + done_move > 0xffffffffull))
+      bad = 1;
+    __syncthreads();
+    if (bad) break;  // workgroup-uniform; nothing past cap was or will be written
+
+    // 4. the data chunks this segment completes (every byte below done_*)
+    const uint64_t end_k = (d0k + done_keep) >> 4, end_m = (d0m + done_move) >> 4;
+    copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, end_k, keep_type, t);
+    next_k = end_k;
+    if (moving) {
+      copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, end_m, move_type, t);
+      next_m = end_m;
     }
   }
-  if (t == 0 && (kTabData + total_keep > job->cap || (moving && kTabData + total_move > job->cap) ||
-                 kTabData + total_keep + total_move > 0xffffffffull))
-    bad = 1;
-  uint32_t rank_keep = ck - n_keep, rank_move = refs_keep + cm - n_move;  // this thread's first record ranks
-#pragma unroll
-  for (uint32_t w = 0; w < kWaves; ++w)
-    if (w < wave) {
-      rank_keep += wsum[2][w];
-      rank_move += wsum[3][w];
-    }
-  uint32_t run_keep = base_keep + ik - sum_keep, run_move = base_move + im - sum_move;  // exclusive
-  uint32_t at[kRefsPerThread];  // each ref's record offset in its image
-#pragma unroll
-  for (uint32_t j = 0; j < kRefsPerThread; ++j) {
-    const bool mv = (to_move >> j) & 1u;
-    at[j] = kTabData + (mv ? run_move : run_keep);
-    if (len[j]) {
-      const uint32_t r = mv ? rank_move++ : rank_keep++;
-      e_end[r] = (mv ? run_move : run_keep) + len[j];
-      e_pos[r] = pos[j];
-    }
-    run_keep += mv ? 0u : len[j];
-    run_move += mv ? len[j] : 0u;
-  }
-  __syncthreads();
   if (bad) {
     if (t == 0) flag(job, SHF_HB_ERR_ARG);
     return;
   }
-
-  // 3. this row in both images (a ref not copied to an image is 0 there: fresh tabs)
-  uint8_t* keep = dst_base + job->keep;
-  uint8_t* move = moving ? dst_base + job->move : nullptr;
-  u32x4* krow = reinterpret_cast<u32x4*>(keep + kTabHdr + (uint64_t)t * kRefsPerThread * 8u);
-  u32x4* mrow = moving ? reinterpret_cast<u32x4*>(move + kTabHdr + (uint64_t)t * kRefsPerThread * 8u) : nullptr;
-#pragma unroll
-  for (uint32_t q = 0; q < kRefsPerThread / 2; ++q) {
-    u32x4 k = {0u, 0u, 0u, 0u}, m = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      const uint32_t j = 2 * q + h;
-      const bool used = len[j] != 0, mv = (to_move >> j) & 1u;
-      const uint32_t a = (used && !mv) ? w0[j] : 0u, b = (used && !mv) ? at[j] : 0u;
-      const uint32_t c = (used && mv) ? w0[j] : 0u, d = (used && mv) ? at[j] : 0u;
-      if (h == 0) {
-        k.x = a, k.y = b, m.x = c, m.y = d;
-      } else {
-        k.z = a, k.w = b, m.z = c, m.w = d;
-      }
-    }
-    *reinterpret_cast<u32x4_a1*>(krow + q) = k;  // 8-B aligned images
-    if (moving) *reinterpret_cast<u32x4_a1*>(mrow + q) = m;
-  }
-
-  // 4. the records: each image's data region as 16-B destination chunks
-  //    (absolute 16-B alignment), consecutive chunks on consecutive lanes, four
-  //    per lane in flight. A chunk's bytes come from the record holding its first
-  //    byte (binary search of the ends) and, where it crosses record ends, the
-  //    next ones; each record's first byte is its SHF_DATA_TYPE, written as the
-  //    job says (shf.c:593-596). Only the images' data bytes are written.
-#ifndef SHFHB_TAB_CHUNKS
-#define SHFHB_TAB_CHUNKS 4
-#endif
-  constexpr uint32_t kChunksPerLane = SHFHB_TAB_CHUNKS;
-#pragma unroll 1
-  for (uint32_t m = 0; m < (moving ? 2u : 1u); ++m) {
-    const uint32_t b0 = m ? refs_keep : 0u, nrec = m ? refs_move : refs_keep;
-    const uint64_t total = m ? total_move : total_keep;
-    if (total == 0) continue;
-    const uint32_t type = m ? job->move_type : job->keep_type;
-    const uint64_t d0 = reinterpret_cast<uintptr_t>((m ? move : keep) + kTabData);  // absolute
-    const uint64_t c0 = d0 >> 4, nchunks = ((d0 + total + 15u) >> 4) - c0;
-    for (uint64_t base = 0; base < nchunks; base += kChunksPerLane * kThreads) {
-      unsigned __int128 v[kChunksPerLane];
-      uint32_t k[kChunksPerLane], lo[kChunksPerLane], hi[kChunksPerLane], st[kChunksPerLane];
-      int64_t a[kChunksPerLane];
-#pragma unroll
-      for (uint32_t q = 0; q < kChunksPerLane; ++q) {
-        const uint64_t i = base + q * kThreads + t;
-        a[q] = (int64_t)((c0 + i) << 4) - (int64_t)d0;  // the chunk's first byte in the image's data
-        lo[q] = a[q] < 0 ? 0u : (uint32_t)a[q];
-        hi[q] = (uint32_t)min<int64_t>(a[q] + 16, (int64_t)total);
-        if (i >= nchunks) hi[q] = lo[q];
-        uint32_t l = 0, h = nrec;  // first record ending past lo
-        while (l < h) {
-          const uint32_t mid = (l + h) >> 1;
-          if (e_end[b0 + mid] > lo[q]) h = mid;
-          else l = mid + 1;
-        }
-        k[q] = b0 + l;
-        if (lo[q] < hi[q]) {
-          st[q] = k[q] > b0 ? e_end[k[q] - 1] : 0u;
-          v[q] = load16(src, src_len, (uint64_t)e_pos[k[q]] + (lo[q] - st[q]));
-        }
-      }
-#pragma unroll
-      for (uint32_t q = 0; q < kChunksPerLane; ++q) {
-        if (lo[q] >= hi[q]) continue;
-        unsigned __int128 out = 0, x = v[q];
-        uint32_t b = lo[q], s0 = st[q], kk = k[q];
-        for (;;) {
-          const uint32_t e = e_end[kk], take = min(e, hi[q]) - b, o = (uint32_t)(b - a[q]);
-          if (b == s0) x = (x & ~(unsigned __int128)0xff) | type;
-          out |= (x & low_bytes128(take)) << (8 * o);
-          b += take;
-          if (b >= hi[q]) break;
-          s0 = e;
-          ++kk;
-          x = load16(src, src_len, e_pos[kk]);
-        }
-        uint8_t* dst = reinterpret_cast<uint8_t*>((c0 + base + q * kThreads + t) << 4);
-        const uint32_t o = (uint32_t)((int64_t)lo[q] - a[q]);  // the chunk's first byte it writes
-        const uint32_t n = hi[q] - lo[q];
-        if (n == 16u) {
-          *reinterpret_cast<u32x4*>(dst) = u32x4{(uint32_t)out, (uint32_t)(out >> 32), (uint32_t)(out >> 64),
-                                                 (uint32_t)(out >> 96)};
-        } else {
-          const unsigned __int128 y = out >> (8 * o);
-          store_partial(dst + o, u32x4{(uint32_t)y, (uint32_t)(y >> 32), (uint32_t)(y >> 64), (uint32_t)(y >> 96)}, n);
-        }
-      }
-    }
-  }
+  // the last partial chunk of each image
+  copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, (d0k + done_keep + 15u) >> 4, keep_type, t);
+  if (moving) copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, (d0m + done_move + 15u) >> 4, move_type, t);
 
   // 5. headers: tab_size (replayed growth), tab_used, tab_refs_used (SHF_TAB_APPEND and
   //    SHF_TAB_REF_COPY both count each copied ref, shf.c:608, :651), free pos, free, data used
   if (wave == 0 || (moving && wave == 1)) {
     const bool m = wave == 1;
-    const uint64_t size = replay_tab_size(e_end + (m ? refs_keep : 0u), m ? refs_move : refs_keep, factor, lane);
+    const uint64_t size = replay_tab_size(m ? LM : LK, m ? refs_move : refs_keep, factor, lane);
     if (lane == 0) {
       uint8_t* img = m ? move : keep;
-      const uint64_t total = m ? total_move : total_keep;
+      const uint64_t total = m ? done_move : done_keep;
       store_u32(img + 0, (uint32_t)size);
       store_u32(img + 4, (uint32_t)(kTabData + total));
       store_u32(img + 8, 2u * (m ? refs_move : refs_keep));
