@@ -211,62 +211,12 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
   }
 }
 
-// Copy the image's records of ranks [r_begin, r_end) (list L; the image's data
-// starts at `data`): 8 lanes per record, each lane 16 B of it per pass (a
-// record over 128 B takes more passes), kRecsPerGroup records per group in
-// flight. A wave's 8 groups take 8 consecutive records, whose destinations are
-// contiguous. The record's first byte is its SHF_DATA_TYPE, written as the job
-// says (shf.c:593-596); a record's last piece is stored exactly.
-#ifndef SHFHB_TAB_RECS
-#define SHFHB_TAB_RECS 2
-#endif
-__device__ void copy_records(const uint8_t* src, uint64_t src_len, const RecList& L, uint32_t r_begin,
-                             uint32_t r_end, uint8_t* data, uint32_t type, uint32_t t) {
-  constexpr uint32_t R = SHFHB_TAB_RECS, kGroups = kThreads / 8;
-  const uint32_t g = t >> 3, i = t & 7u;
-  for (uint32_t r0 = r_begin + g; r0 < r_end; r0 += R * kGroups) {
-    uint32_t s[R], len[R], sp[R];
-    u32x4 x[R];
-#pragma unroll
-    for (uint32_t q = 0; q < R; ++q) {
-      const uint32_t r = r0 + q * kGroups;
-      len[q] = 0;
-      if (r < r_end) {
-        s[q] = r ? L.end(r - 1) : 0u;
-        len[q] = L.end(r) - s[q];
-        sp[q] = L.pos(r);
-      }
-      if (16u * i < len[q]) {
-        const unsigned __int128 v = load16(src, src_len, (uint64_t)sp[q] + 16u * i);
-        x[q] = u32x4{(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)};
-      }
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < R; ++q) {
-      for (uint32_t off = 16u * i; off < len[q]; off += 128u) {
-        u32x4 v = x[q];
-        if (off != 16u * i) {  // a record over 128 B: its next pass
-          const unsigned __int128 w = load16(src, src_len, (uint64_t)sp[q] + off);
-          v = u32x4{(uint32_t)w, (uint32_t)(w >> 32), (uint32_t)(w >> 64), (uint32_t)(w >> 96)};
-        }
-        if (off == 0) v.x = (v.x & ~0xffu) | type;
-        uint8_t* d = data + s[q] + off;
-        if (off + 16u <= len[q]) *reinterpret_cast<u32x4_a1*>(d) = v;
-        else store_partial(d, v, len[q] - off);
-      }
-    }
-  }
-}
-
 }  // namespace
 
 // Segments of refs processed in order: each reads its refs' length words and
 // copies its records while the lines those reads pulled in are still in L2 /
 // the Infinity Cache (one pass over the whole tab's lengths first would evict
 // them before the copy at 2 tabs per CU: the data are read twice from HBM).
-#ifndef SHFHB_TAB_BYREC
-#define SHFHB_TAB_BYREC 0  // records copied by 8-lane groups instead of 16-B destination chunks
-#endif
 #ifndef SHFHB_TAB_SEGS
 #define SHFHB_TAB_SEGS 4
 #endif
@@ -421,12 +371,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     __syncthreads();
     if (bad) break;  // workgroup-uniform; nothing past cap was or will be written
 
-    // 4. this segment's records
-#if SHFHB_TAB_BYREC
-    copy_records(src, src_len, LK, refs_keep - (uint32_t)seg_tot[2], refs_keep, keep + kTabData, keep_type, t);
-    if (moving)
-      copy_records(src, src_len, LM, refs_move - (uint32_t)seg_tot[3], refs_move, move + kTabData, move_type, t);
-#else  // the data chunks this segment completes (every byte below done_*)
+    // 4. the data chunks this segment completes (every byte below done_*)
     const uint64_t end_k = (d0k + done_keep) >> 4, end_m = (d0m + done_move) >> 4;
     copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, end_k, keep_type, t);
     next_k = end_k;
@@ -434,16 +379,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, end_m, move_type, t);
       next_m = end_m;
     }
-#endif
   }
   if (bad) {
     if (t == 0) flag(job, SHF_HB_ERR_ARG);
     return;
   }
-#if !SHFHB_TAB_BYREC  // the last partial chunk of each image
+  // the last partial chunk of each image
   copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, (d0k + done_keep + 15u) >> 4, keep_type, t);
   if (moving) copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, (d0m + done_move + 15u) >> 4, move_type, t);
-#endif
 
   // 5. headers: tab_size (replayed growth), tab_used, tab_refs_used (SHF_TAB_APPEND and
   //    SHF_TAB_REF_COPY both count each copied ref, shf.c:608, :651), free pos, free, data used
