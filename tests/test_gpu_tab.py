@@ -157,3 +157,29 @@ def test_host_memory_entry_point(hb, dev):
                                 m.ctypes.data, 1, ctypes.byref(prm), hb.MEM_HOST)
     assert rc == hb.OK and jobs[0].status == hb.OK
     tabcheck.check_capture(cap, dst[:size], dst[size:], 16)
+
+
+@pytest.mark.parametrize("n_refs,kl,vl,seed", [
+    (8192, (0, 0), (0, 0), 1),        # every ref used, minimal 9-B records (chunks straddle several)
+    (300, (1000, 5000), (0, 3000), 2),  # few, large records (kilobytes: many chunks each)
+    (4500, (16, 64), (8, 128), 3),      # the bench's shape
+    (1, (5, 5), (5, 5), 4),             # a single record
+    (0, (8, 8), (8, 8), 5),             # an empty tab
+])
+def test_synthetic_tabs_match_oracle(hb, dev, oracle, n_refs, kl, vl, seed):
+    """Synthetic tabs (sharedhashfile_amd/tabgen.py) of very different shapes,
+    parted and shrunk in one launch, against the CPU oracle: the kernel's
+    segment boundaries, record lists and chunk gathers at their extremes."""
+    from sharedhashfile_amd.tabgen import synth_tab
+
+    img, m, old = synth_tab(seed, n_refs=n_refs, key_lo=kl[0], key_hi=kl[1], val_lo=vl[0], val_hi=vl[1])
+    new = (old + 1000) % 2048
+    m2 = hb.tab_part_redirect(m, old, new)
+    got = hb.tab_copy([img, img], [m2, m2], [new, hb.TAB_NONE], keep_type=0x3E, move_type=0xBE)
+    for (keep, move), tn in zip(got, [new, hb.TAB_NONE]):
+        wk, wm = oracle.tab_split(img, m2, tn, cap=keep.size, keep_type=0x3E, move_type=0xBE)
+        assert np.array_equal(keep, wk)
+        if tn == hb.TAB_NONE:
+            assert move is None
+        else:
+            assert np.array_equal(move, wm)
