@@ -266,7 +266,8 @@ typedef struct shf_tab_job {
     uint16_t tab_new;   /* the new tab's number, or SHF_TAB_NONE: shrink only */
     uint8_t keep_type;  /* SHF_DATA_TYPE byte written at each record copied to keep (0x3e: key and value STR32) */
     uint8_t move_type;  /* ... copied to move */
-    int32_t status;     /* out: SHF_HB_OK, or SHF_HB_ERR_ARG (out of range, corrupt record, output too small) */
+    int32_t status;     /* out: SHF_HB_OK, or SHF_HB_ERR_ARG (out of range, corrupt record, output too small);
+                           after ERR_ARG the job's output images are unspecified (never written past cap) */
     uint32_t reserved;
 } shf_tab_job;
 
