@@ -753,84 +753,6 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
   return s;
 }
 
-#ifndef SHFHB_PP_SPLIT
-#define SHFHB_PP_SPLIT 0
-#endif
-// A staged tile hashed in two passes by its wave (every lane calls it; len 0
-// for lanes without a key): first the k1/k2 mixes of all the tile's full
-// blocks (murmurhash3.c:97, :101), spread evenly over the lanes (lane l takes
-// blocks [l B/64, (l+1) B/64) of the tile's B blocks in key order) and written
-// back over the blocks; then each lane runs its own key's serial h1/h2 chain
-// over the mixed blocks, its tail (raw bytes, untouched) and fmix. The lanes'
-// unequal key lengths then cost only the chain's share of a block.
-__device__ __forceinline__ State hash_tile_split(uint32_t* lds, uint32_t tbl_byte, uint32_t p, uint32_t len,
-                                                 uint32_t seed, uint32_t lane) {
-  typedef __attribute__((address_space(3))) uint8_t lds_u8w;
-  typedef __attribute__((address_space(3))) u32x4_a1 lds_u32x4_a1w;
-  const uint32_t nb = len >> 4;
-  // per-key table after the span: window byte | block count << 16 (p < 64 KiB, nb < 64 Ki)
-  uint32_t* tbl = lds + (tbl_byte >> 2);
-  tbl[lane] = p | (nb << 16);
-  tbl[64 + lane] = 0u;  // sentinel past the last key
-  uint32_t incl = nb;  // inclusive prefix of the block counts over the lanes
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t u = (uint32_t)__shfl_up((int)incl, d);
-    if (lane >= d) incl += u;
-  }
-  const uint32_t P = incl - nb;
-  const uint32_t B = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  const uint32_t per = (B + 63u) >> 6;
-  const uint32_t b0 = min(lane * per, B), b1 = min(b0 + per, B);
-  // the key holding block b0: the last lane whose prefix is <= b0 (empty keys share a prefix with the next)
-  uint32_t k = 0;
-#pragma unroll
-  for (uint32_t step = 32; step >= 1; step >>= 1)
-    if ((uint32_t)__shfl((int)P, (int)(k + step)) <= b0) k += step;
-  uint32_t j = b0 - (uint32_t)__shfl((int)P, (int)k);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint32_t cur = tbl[k], nxt = tbl[k + 1];
-  for (uint32_t it = 0; it < per; ++it) {
-    if (b0 + it < b1) {
-      if (j >= (cur >> 16)) {  // this key's blocks are done: the next key with any
-        do {
-          ++k;
-          cur = nxt;
-          nxt = tbl[k + 1];
-        } while ((cur >> 16) == 0 && k < 63u);
-        j = 0;
-      }
-      const uint32_t at = (cur & 0xffffu) + 16u * j;
-      const u32x4 v = lds_read16(lds, at);
-      const uint64_t m1 = mix_k1(pack64(v.x, v.y)), m2 = mix_k2(pack64(v.z, v.w));
-      *(lds_u32x4_a1w*)((lds_u8w*)lds + at) =
-          u32x4{(uint32_t)m1, (uint32_t)(m1 >> 32), (uint32_t)m2, (uint32_t)(m2 >> 32)};
-      ++j;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // the chains: block j's mixed words beside block j+1's read
-  State s{seed, seed};
-  u32x4 c = lds_read16(lds, p);
-  for (uint32_t jj = 0; jj < nb; ++jj) {
-    const u32x4 n2 = lds_read16(lds, p + 16u * jj + 16u);
-    chain_block(s, pack64(c.x, c.y), pack64(c.z, c.w));
-    c = n2;
-  }
-  const uint32_t rem = len & 15u;
-  if (rem) {  // c holds the tail's raw bytes
-    const uint64_t t1 = pack64(c.x, c.y) & low_bytes_mask(rem);
-    const uint64_t t2 = rem > 8 ? (pack64(c.z, c.w) & low_bytes_mask(rem - 8)) : 0ull;
-    tail_block(s, t1, t2, rem);
-  }
-  finish(s, len);
-  return s;
-}
-
 // ---------------------------------------------------------------------------
 // Round kernel: variable-length keys, streamed 128 B per key per round.
 // One wave (= one workgroup) owns 64 consecutive keys. Round r stages, for
@@ -1075,22 +997,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     if (wave == phase && has) {
       if (staged) {
-#if SHFHB_PP_SPLIT
-        const uint32_t tb = (ti.span16 + 15u) & ~15u;  // the key table's byte in the window
-        if (tb + 512u <= kSpanAlloc) {
-          const uint32_t p = ti.valid ? (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base) : 0u;
-          const State st = hash_tile_split(span_lds, tb, p, ti.valid ? ti.len : 0u, seed, lane);
-          if (ti.valid) store_result<OUT>(sink, ti.key, st);
-        } else if (ti.valid) {
-          const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-          store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, p, ti.len, seed));
-        }
-#else
         if (ti.valid) {
           const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
           store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, p, ti.len, seed));
         }
-#endif
       } else {
         span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
       }
