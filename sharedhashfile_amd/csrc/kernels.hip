@@ -354,55 +354,6 @@ __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint
   return s;
 }
 
-// hash_bytes from block j0 on, with the chain state after blocks [0, j0).
-__device__ __forceinline__ State hash_bytes_from(const uint8_t* p, uint32_t len, uint32_t j0, State s) {
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
-  const uint32_t sh = (uint32_t)(addr & 3u);
-  const g_u32* w = reinterpret_cast<const g_u32*>(addr - sh);
-  const uint32_t nblocks = len >> 4;
-  uint32_t j = j0;
-  for (; j + 4 <= nblocks; j += 4) {  // 64-B burst per lane
-    const g_u32x4_a4* v = reinterpret_cast<const g_u32x4_a4*>(w + 4 * j);
-    const u32x4 a = v[0], b = v[1], c = v[2], d = v[3];
-    const uint32_t e = sh ? w[4 * j + 16] : 0u;
-    const uint32_t x[17] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t d0 = __builtin_amdgcn_alignbyte(x[4 * q + 1], x[4 * q + 0], sh);
-      const uint32_t d1 = __builtin_amdgcn_alignbyte(x[4 * q + 2], x[4 * q + 1], sh);
-      const uint32_t d2 = __builtin_amdgcn_alignbyte(x[4 * q + 3], x[4 * q + 2], sh);
-      const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4 * q + 4], x[4 * q + 3], sh);
-      body_block(s, pack64(d0, d1), pack64(d2, d3));
-    }
-  }
-  for (; j < nblocks; ++j) {
-    const u32x4 a = *reinterpret_cast<const g_u32x4_a4*>(w + 4 * j);
-    const uint32_t e = sh ? w[4 * j + 4] : 0u;
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(a.w, a.z, sh);
-    const uint32_t d3 = __builtin_amdgcn_alignbyte(e, a.w, sh);
-    body_block(s, pack64(d0, d1), pack64(d2, d3));
-  }
-  const uint32_t rem = len & 15u;
-  if (rem) {
-    const g_u32* t = w + 4 * nblocks;
-    const uint32_t need = sh + rem;
-    uint32_t x[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) x[q] = (4u * q < need) ? t[q] : 0u;
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
-    const uint32_t d3 = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
-    const uint64_t t1 = pack64(d0, d1) & low_bytes_mask(rem);
-    const uint64_t t2 = rem > 8 ? (pack64(d2, d3) & low_bytes_mask(rem - 8)) : 0ull;
-    tail_block(s, t1, t2, rem);
-  }
-  finish(s, len);
-  return s;
-}
-
 #ifndef SHFHB_GENERIC_GRID_CAP
 #define SHFHB_GENERIC_GRID_CAP (1u << 20)  // one key per lane: 5.57 vs 5.19 TB/s at 32-B keys
 #endif
@@ -756,9 +707,6 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
 #ifndef SHFHB_LDS_UNALIGNED
 #define SHFHB_LDS_UNALIGNED 1  // variable-length k_span: U[8,512] B keys +4-8 % (profiles/r2/ab_span/)
 #endif
-#ifndef SHFHB_PP_TAILT
-#define SHFHB_PP_TAILT 0  // k_span_pp: blocks per key hashed in the window before it is handed on (0: all)
-#endif
 #ifndef SHFHB_SPAN_PINGPONG
 #define SHFHB_SPAN_PINGPONG 1  // k_span_pp for variable-length windows over 10 KiB
 #endif
@@ -803,35 +751,6 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
   }
   finish(s, len);
   return s;
-}
-
-// hash_lds_u for at most `cap_blocks` blocks: a key that ends within them is
-// finished (returns true); a longer one returns its chain state after them.
-__device__ __forceinline__ bool hash_lds_head(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed,
-                                              uint32_t cap_blocks, State& s) {
-  const uint32_t nblocks = len >> 4, run = min(nblocks, cap_blocks);
-  s = State{seed, seed};
-  u32x4 cur = lds_read16(lds, p);
-  u32x4 nxt = lds_read16(lds, p + 16u);
-  uint64_t m1 = mix_k1(pack64(cur.x, cur.y)), m2 = mix_k2(pack64(cur.z, cur.w));
-  for (uint32_t j = 0; j < run; ++j) {
-    const u32x4 nn = lds_read16(lds, p + 16u * j + 32u);
-    const uint64_t n1 = mix_k1(pack64(nxt.x, nxt.y)), n2 = mix_k2(pack64(nxt.z, nxt.w));
-    chain_block(s, m1, m2);
-    m1 = n1;
-    m2 = n2;
-    cur = nxt;
-    nxt = nn;
-  }
-  if (nblocks > cap_blocks) return false;
-  const uint32_t rem = len & 15u;
-  if (rem) {
-    const uint64_t t1 = pack64(cur.x, cur.y) & low_bytes_mask(rem);
-    const uint64_t t2 = rem > 8 ? (pack64(cur.z, cur.w) & low_bytes_mask(rem - 8)) : 0ull;
-    tail_block(s, t1, t2, rem);
-  }
-  finish(s, len);
-  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -1072,33 +991,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool staged = has && !bad && ti.span16 <= cap;
   u32x4 reg[PIECES];
   if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-#if SHFHB_PP_TAILT
-  // Each wave hashes at most SHFHB_PP_TAILT blocks per key in the window, then
-  // hands the window on; a longer key's remaining blocks are hashed afterwards
-  // straight from memory (its span's lines were loaded a moment ago), while the
-  // other wave uses the window.
-  State st{seed, seed};
-  bool done = true;
-#pragma unroll
-  for (uint32_t phase = 0; phase < 2; ++phase) {
-    if (wave == phase && staged) span_stage<PIECES>(span_lds, reg, ti.span16, lane);
-    __syncthreads();
-    if (wave == phase && has) {
-      if (staged) {
-        if (ti.valid) {
-          const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-          done = hash_lds_head(span_lds, p, ti.len, seed, SHFHB_PP_TAILT, st);
-          if (done) store_result<OUT>(sink, ti.key, st);
-        }
-      } else {
-        span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-      }
-    }
-    if (phase == 0) __syncthreads();
-  }
-  if (staged && ti.valid && !done)
-    store_result<OUT>(sink, ti.key, hash_bytes_from(bytes + ti.start, ti.len, SHFHB_PP_TAILT, st));
-#else
 #pragma unroll
   for (uint32_t phase = 0; phase < 2; ++phase) {
     if (wave == phase && staged) span_stage<PIECES>(span_lds, reg, ti.span16, lane);
@@ -1115,7 +1007,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
     __syncthreads();
   }
-#endif
 }
 
 // ---------------------------------------------------------------------------
