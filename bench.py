@@ -892,7 +892,7 @@ def run_rank(args):
             line["rehearsal"] = True
             line["rehearsal_note"] = "%d ranks shared %d GPU(s) (--allow-shared-gpu): throughput is not a " \
                                      "multi-GPU measurement" % (world, n_gpus)
-        print(json.dumps(line), flush=True)
+        os.write(args.json_fd, (json.dumps(line) + "\n").encode())
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -908,6 +908,12 @@ def main(argv=None):
             return launch_ranks(argv, n)
     elif args.gpus is not None and args.gpus != int(env_world):
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus, env_world))
+    # stdout carries exactly one JSON line (rank 0's): whatever else writes to
+    # fd 1 in a rank process (gloo's connection notices, library chatter) goes
+    # to stderr
+    sys.stdout.flush()
+    args.json_fd = os.dup(1)
+    os.dup2(2, 1)
     run_rank(args)
     return 0
 

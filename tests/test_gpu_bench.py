@@ -45,7 +45,9 @@ def test_two_ranks_refused_on_one_gpu():
 def test_two_rank_rehearsal_shards_configs4():
     p = _run(["--allow-shared-gpu"])
     assert p.returncode == 0, p.stderr[-3000:]
-    line = json.loads(p.stdout.strip().splitlines()[-1])
+    out = p.stdout.strip().splitlines()
+    assert len(out) == 1, out  # stdout is the JSON line alone (gloo's notices and the like go to stderr)
+    line = json.loads(out[0])
     ndev = torch.cuda.device_count()
     assert line["ranks"] == 2
     assert line["n_gpus"] == min(2, ndev)
