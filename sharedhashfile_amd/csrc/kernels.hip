@@ -633,6 +633,21 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
       reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
+// span_fetch that defines every piece (zero past the span), so that a loop
+// carrying `reg` does not keep the previous tile's pieces live.
+template <int PIECES>
+__device__ __forceinline__ void span_fetch_all(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(span16);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
+#pragma unroll
+  for (int q = 0; q < PIECES; ++q)
+    reg[q] = (uint32_t)q * 1024u < nb ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2)
+                                      : u32x4{0u, 0u, 0u, 0u};
+}
+
 // Stage the fetched pieces that hold span bytes (lanes past the span's end
 // write nothing: the window may be exactly the span plus its read slack).
 template <int PIECES>
@@ -954,7 +969,8 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
 // Ping-pong span kernel (variable-length keys): two waves share one LDS
 // window and take turns. Both load their tile's span into registers at once;
 // wave 0 stages and hashes its tile while wave 1's span is still arriving,
-// then wave 1 stages and hashes. A window then holds bytes only while they are
+// then one LDS-only barrier hands the window to wave 1, which stages and
+// hashes. A window then holds bytes only while they are
 // staged or hashed (one HBM latency per two tiles instead of one per tile),
 // and a CU keeps twice as many hashing waves (4 per SIMD) for the same LDS.
 // U[8,512] B keys: +10 %, all-260 B: +15 %, U[200,400] B: +12 % over k_span
@@ -966,6 +982,57 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
 // next span prefetched into registers during the hash measured 0-10 % slower
 // than k_span: neither kept, git history.)
 // ---------------------------------------------------------------------------
+// Workgroup barrier that waits for this wave's LDS accesses only. (A
+// __syncthreads() also waits for every global store in flight, vmcnt(0): in
+// k_span_pp that put the round trip of wave 0's result stores between its hash
+// and wave 1's, profiles/r2/ab_span/ab_handoff2 vs ab_sort.)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Orders this wave's LDS writes before its own later LDS reads.
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifndef SHFHB_PP_SORT
+#define SHFHB_PP_SORT 0  // k_span_pp: lanes take the tile's keys in block-count order (experiment)
+#endif
+
+// Hash the staged tile: lane l hashes key l, or (SHFHB_PP_SORT) the key of
+// rank l by block count, so that finished lanes gather in the low lanes.
+template <int OUT>
+__device__ __forceinline__ void span_hash_tile(const uint32_t* lds, const uint8_t* bytes, const SpanTile<true>& ti,
+                                               uint32_t lane, uint32_t seed, const Sink& sink) {
+#if SHFHB_PP_SORT
+  const uint32_t nbk = ti.valid ? min(ti.len >> 4, (1u << 25) - 1u) : 0u;
+  uint32_t v = (nbk << 6) | lane;
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)j);
+      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      v = keep_min ? min(v, o) : max(v, o);
+    }
+  }
+  const int src = (int)(v & 63u);
+  const uint64_t start = (uint64_t)(uint32_t)__shfl((int)(uint32_t)ti.start, src) |
+                         ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ti.start >> 32), src) << 32);
+  const uint32_t len = (uint32_t)__shfl((int)ti.len, src);
+  const bool valid = __shfl((int)ti.valid, src) != 0;
+  const uint64_t key = ti.key - lane + (uint32_t)src;
+#else
+  const uint64_t start = ti.start, key = ti.key;
+  const uint32_t len = ti.len;
+  const bool valid = ti.valid;
+#endif
+  if (valid) {
+    const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + start - ti.base);
+    store_result<OUT>(sink, key, hash_lds_u(lds, p, len, seed));
+  }
+}
+
 template <int OUT>
 __device__ __forceinline__ void span_tile_from_hbm(const uint8_t* bytes, uint64_t off_base, uint64_t n,
                                                    const SpanRaw& raw, uint32_t lane, uint32_t seed, const Sink& sink) {
@@ -991,22 +1058,232 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool staged = has && !bad && ti.span16 <= cap;
   u32x4 reg[PIECES];
   if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-#pragma unroll
-  for (uint32_t phase = 0; phase < 2; ++phase) {
-    if (wave == phase && staged) span_stage<PIECES>(span_lds, reg, ti.span16, lane);
-    __syncthreads();
-    if (wave == phase && has) {
-      if (staged) {
-        if (ti.valid) {
-          const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-          store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, p, ti.len, seed));
-        }
-      } else {
-        span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-      }
-    }
-    __syncthreads();
+  // Wave 0 stages and hashes; one barrier hands the window to wave 1, which
+  // stages and hashes in turn (a wave's own LDS writes and reads are ordered
+  // by a wave-level fence). One barrier instead of the four of two
+  // stage/hash phases: U[8,512] +1.7 %, all-260 B +10.6 %, U[200,400] +4.7 %
+  // (profiles/r2/ab_span/ab_handoff2, "t32").
+  if (wave == 0 && staged) {
+    span_stage<PIECES>(span_lds, reg, ti.span16, lane);
+    wave_lds_fence();
+    span_hash_tile<OUT>(span_lds, bytes, ti, lane, seed, sink);
   }
+  lds_barrier();  // wave 0 is done with the window (its result stores may still be in flight)
+  if (wave == 1 && staged) {
+    span_stage<PIECES>(span_lds, reg, ti.span16, lane);
+    wave_lds_fence();
+    span_hash_tile<OUT>(span_lds, bytes, ti, lane, seed, sink);
+  }
+  if (has && !staged) span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
+}
+
+#ifndef SHFHB_PQ_K
+#define SHFHB_PQ_K 0  // k_span_pq: tiles per wave (0: k_span_pp, one tile per wave)
+#endif
+#ifndef SHFHB_PQ_OFFPF
+#define SHFHB_PQ_OFFPF 0  // k_span_pq: load the next tile's offsets before hashing this one
+#endif
+
+// Relay ping-pong: k_span_pp's two waves and one window, but each wave
+// hashes K tiles in turn (tiles 2j + wave of the workgroup's 2K), fetching its
+// next span into registers right after each hash, while the partner hashes.
+// The window then waits for HBM once per 2K tiles. The hand-overs are
+// LDS-only barriers: a wave's span fetch and result stores stay in flight.
+// One wave's part of k_span_pq (FIRST: wave 0, which hashes first). Written
+// per wave so that a wave's held span is not live across its own hash.
+template <int OUT, int PIECES, int K, bool FIRST>
+__device__ __forceinline__ void span_pq_wave(const uint8_t* bytes, const uint64_t* offsets, uint64_t off_base,
+                                             uint64_t n, uint32_t seed, uint32_t cap, const Sink& sink,
+                                             uint32_t* span_lds, uint32_t lane) {
+  const uint64_t ntiles = (n + 63) / 64;
+  uint64_t t = (uint64_t)blockIdx.x * (2u * K) + (FIRST ? 0u : 1u);
+  SpanRaw raw = span_load<true>(offsets, n, t, lane);
+  bool has = t < ntiles;
+  bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
+  SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
+  bool staged = has && !bad && ti.span16 <= cap;
+  u32x4 reg[PIECES];
+  span_fetch_all<PIECES>(reg, staged ? ti.base : 0u, staged ? ti.span16 : 0u, lane);
+#if SHFHB_PQ_OFFPF
+  SpanRaw nraw = span_load<true>(offsets, n, t + 2u, lane);
+#endif
+  for (uint32_t j = 0; j < K; ++j) {
+    if (!FIRST) lds_barrier();  // the partner is done with the window
+    if (staged) {
+      span_stage<PIECES>(span_lds, reg, ti.span16, lane);
+      wave_lds_fence();
+      span_hash_tile<OUT>(span_lds, bytes, ti, lane, seed, sink);
+    } else if (has) {  // rare: offsets re-read rather than held across the loop
+      span_tile_from_hbm<OUT>(bytes, off_base, n, span_load<true>(offsets, n, t, lane), lane, seed, sink);
+    }
+    if (j + 1 < K) {  // this wave's next tile, in flight while the partner hashes
+      t += 2u;
+#if SHFHB_PQ_OFFPF
+      raw = nraw;
+      if (j + 2 < K) nraw = span_load<true>(offsets, n, t + 2u, lane);
+#else
+      raw = span_load<true>(offsets, n, t, lane);
+#endif
+      has = t < ntiles;
+      bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
+      ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
+      staged = has && !bad && ti.span16 <= cap;
+      span_fetch_all<PIECES>(reg, staged ? ti.base : 0u, staged ? ti.span16 : 0u, lane);
+    }
+    if (FIRST || j + 1 < K) lds_barrier();  // hand the window over
+    if (FIRST && j + 1 < K) lds_barrier();  // and wait for it back
+  }
+}
+
+template <int OUT, int PIECES, int K>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_span_pq(
+    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
+    uint32_t seed, uint32_t cap, Sink sink) {
+  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
+  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (__builtin_amdgcn_readfirstlane(wave) == 0)
+    span_pq_wave<OUT, PIECES, K, true>(bytes, offsets, off_base, n, seed, cap, sink, span_lds, lane);
+  else
+    span_pq_wave<OUT, PIECES, K, false>(bytes, offsets, off_base, n, seed, cap, sink, span_lds, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Pair-sorted span kernel (variable-length keys): a wave's block loop runs to
+// the longest key of its 64, so on U[8,512] B keys lanes idle through half of
+// it. Here two waves share a 128-key tile (one contiguous span, one 40-KiB
+// window) and split its keys by length: each sorts its own 64 block counts
+// (bitonic, in-wave shuffles; ascending in wave 0, descending in wave 1), one
+// exchange of the two sorted halves through LDS leaves the 64 shorter keys in
+// wave 0 and the 64 longer in wave 1 (the bitonic split), and each lane hashes
+// the key it was given. A tile's loops then run to about the median and the
+// maximum block count instead of twice the maximum. A workgroup holds two such
+// pairs of waves, taking turns on the window as in k_span_pp (the second
+// pair's spans wait in registers).
+// ---------------------------------------------------------------------------
+#ifndef SHFHB_SPAN_PAIRSORT
+#define SHFHB_SPAN_PAIRSORT 0
+#endif
+constexpr uint32_t kPsAlloc = 40u * 1024u;                      // 4 workgroups per CU
+constexpr uint32_t kPsTblBytes = 128u * 4u;                     // per key: u16 start in the span | u16 length << 16
+constexpr uint32_t kPsXchBytes = 128u * 4u;                     // the sorted halves' exchange
+constexpr uint32_t kPsCap = kPsAlloc - kSpanPad - kPsTblBytes - kPsXchBytes;  // span bytes (39360)
+constexpr int kPsPieces = 20;                                   // 1-KiB pieces fetched per wave (2 x 20 >= kPsCap)
+
+// Bitonic sort of one value per lane across the wave (ascending, or descending).
+__device__ __forceinline__ uint32_t wave_sort_u32(uint32_t v, uint32_t lane, bool desc) {
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)j);
+      const bool keep_min = (((lane & j) == 0) == ((lane & k) == 0)) != desc;
+      v = keep_min ? min(v, o) : max(v, o);
+    }
+  }
+  return v;
+}
+
+// One wave's part of a k_span_ps workgroup. SECOND: a wave of the second pair
+// (its span waits in registers while the first pair hashes). Written per pair
+// so that a held span is not live across the same wave's hash.
+template <int OUT, bool SECOND>
+__device__ __forceinline__ void span_ps_wave(const uint8_t* bytes, const uint64_t* offsets, uint64_t off_base,
+                                             uint64_t n, uint32_t seed, const Sink& sink, uint32_t* lds, uint32_t h,
+                                             uint32_t lane) {
+  uint32_t* tbl = lds + (kPsCap + kSpanPad) / 4u;
+  uint32_t* xch = tbl + 128u;
+  const uint64_t k0 = ((uint64_t)blockIdx.x * 2u + (SECOND ? 1u : 0u)) * 128u;
+  const bool has = k0 < n;
+  const uint32_t kn = has ? (uint32_t)min<uint64_t>(128u, n - k0) : 0u;
+  // this lane's key and the other half's (each wave checks all 128 keys' offsets)
+  const uint32_t my = 64u * h + lane, ot = 64u * (1u - h) + lane;
+  uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  if (my < kn) {
+    a0 = offsets[k0 + my];
+    a1 = offsets[k0 + my + 1];
+  }
+  if (ot < kn) {
+    b0 = offsets[k0 + ot];
+    b1 = offsets[k0 + ot + 1];
+  }
+  const bool bad = __ballot(var_key_bad(a0, a1) || var_key_bad(b0, b1)) != 0;
+  uint64_t base = 0;
+  uint32_t span16 = 0;
+  if (has && !bad) {
+    // the readlane builtins return a signed int: widen through uint32_t
+    const uint64_t f = h == 0 ? a0 : b0;
+    const uint64_t e = ((kn - 1u) >> 6) == h ? a1 : b1;
+    const uint32_t el = (kn - 1u) & 63u;
+    const uint64_t first = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)f) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32);
+    const uint64_t end = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)e, el) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), el) << 32);
+    if (end > first) {
+      const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
+      base = (b + (first - off_base)) & ~(uint64_t)15;
+      const uint64_t span = ((b + (end - off_base) + 15u) & ~(uint64_t)15) - base;
+      span16 = span > 0xffffffffull ? 0xffffffffu : (uint32_t)span;
+    }
+  }
+  const bool staged = has && !bad && span16 <= kPsCap;
+  u32x4 reg[kPsPieces];
+  if (staged) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(span16);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < kPsPieces; ++q) {
+      const uint32_t at = (kPsPieces * h + (uint32_t)q) * 1024u;
+      reg[q] = at < nb ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, at + lane * 16u, 0, 2 /* nt */)
+                       : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  uint32_t v = 0;
+  if (SECOND) {
+    lds_barrier();  // the first pair's exchange
+    lds_barrier();  // the first pair is done with the window
+  }
+  if (staged) {
+#pragma unroll
+    for (int q = 0; q < kPsPieces; ++q) {
+      const uint32_t at = (kPsPieces * h + (uint32_t)q) * 1024u + lane * 16u;
+      if (at < span16) reinterpret_cast<u32x4*>(lds)[at / 16u] = reg[q];
+    }
+    const bool valid = my < kn;
+    const uint32_t len = valid ? (uint32_t)(a1 - a0) : 0u;
+    const uint32_t p = valid ? (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + (a0 - off_base) - base) : 0u;
+    tbl[my] = p | (len << 16);  // p, len < kPsCap < 2^16
+    v = wave_sort_u32(((len >> 4) << 7) | my, lane, h != 0);
+    xch[my] = v;
+  }
+  lds_barrier();  // this pair's halves staged and sorted
+  if (staged) {
+    const uint32_t o = xch[64u * (1u - h) + lane];
+    const uint32_t idx = (h == 0 ? min(v, o) : max(v, o)) & 127u;
+    const uint32_t e = tbl[idx];
+    if (idx < kn) store_result<OUT>(sink, k0 + idx, hash_lds_u(lds, e & 0xffffu, e >> 16, seed));
+  } else if (my < kn) {  // a bad key or a span over the window: this lane's own key from HBM
+    if (var_key_bad(a0, a1)) flag_bad_key(sink);
+    else store_result<OUT>(sink, k0 + my, hash_bytes(bytes + (a0 - off_base), (uint32_t)(a1 - a0), seed));
+  }
+  if (!SECOND) {
+    lds_barrier();  // done with the window
+    lds_barrier();  // (the second pair's exchange)
+  }
+}
+
+template <int OUT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_span_ps(
+    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
+    uint32_t seed, Sink sink) {
+  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
+  extern __shared__ __attribute__((aligned(16))) uint32_t ps_lds[];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (wave < 2) span_ps_wave<OUT, false>(bytes, offsets, off_base, n, seed, sink, ps_lds, wave & 1u, lane);
+  else span_ps_wave<OUT, true>(bytes, offsets, off_base, n, seed, sink, ps_lds, wave & 1u, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1079,8 +1356,26 @@ static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* of
   const uint64_t tiles = (n + 63) / 64;
   const uint64_t wgs = (tiles + 1) / 2;
   if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
+#if SHFHB_PQ_K
+  {
+    const uint64_t g = (tiles + 2u * SHFHB_PQ_K - 1) / (2u * SHFHB_PQ_K);
+    hipLaunchKernelGGL((k_span_pq<OUT, kSpanPiecesMax, SHFHB_PQ_K>), dim3((unsigned)g), dim3(128), kSpanAlloc, st,
+                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((k_span_pp<OUT, kSpanPiecesMax>), dim3((unsigned)wgs), dim3(128), kSpanAlloc, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
+  return hipGetLastError();
+}
+
+template <int OUT>
+static hipError_t launch_var_span_pairsort(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
+                                           uint32_t seed, const Sink& sink, hipStream_t st) {
+  const uint64_t wgs = (n + 255) / 256;  // two 128-key tiles per workgroup
+  if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_span_ps<OUT>, dim3((unsigned)wgs), dim3(256), kPsAlloc, st,
+                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, sink);
   return hipGetLastError();
 }
 
@@ -1109,6 +1404,11 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
                               uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0) {
   if constexpr (VAR) {
     const double need = key_bytes && n ? 64.0 * (double)key_bytes / (double)n * 1.1 + 512.0 + kSpanPad : 1e30;
+    // 128-key tiles whose spans fit 40 KiB (config D's U[8,512] B keys): pair-sorted
+    if constexpr (OUT != kOutProbe)
+      if (SHFHB_SPAN_PAIRSORT && key_bytes && n && 128.0 * (double)key_bytes / (double)n * 1.1 + 512.0 <= kPsCap &&
+          need > 10240.0 + kSpanPad)
+        return launch_var_span_pairsort<OUT>(bytes, offsets, off_base, n, seed, sink, st);
     // windows over 10 KiB (config D's U[8,512] B keys): two waves per window
     if constexpr (OUT != kOutProbe)
       if (SHFHB_SPAN_PINGPONG && need > 10240.0 + kSpanPad)

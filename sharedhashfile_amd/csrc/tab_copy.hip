@@ -224,6 +224,20 @@ constexpr uint32_t kSegs = SHFHB_TAB_SEGS;
 constexpr uint32_t kSegRefs = kTabRefs / kSegs;           // 2048
 constexpr uint32_t kSlabs = kSegRefs / kThreads;          // 4: ref = seg * 2048 + slab * 512 + thread
 
+#ifndef SHFHB_TAB_LDS_BARRIER
+#define SHFHB_TAB_LDS_BARRIER 1
+#endif
+// The segment loop's barriers guard LDS only (the scan sums, the record
+// lists, `bad`): wait for this wave's LDS accesses, not for its row and chunk
+// stores still in flight as __syncthreads() would (vmcnt(0)).
+__device__ __forceinline__ void seg_barrier() {
+#if SHFHB_TAB_LDS_BARRIER
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_tab_split(const uint8_t* __restrict__ src_base, uint64_t src_bytes,
                                                         uint8_t* dst_base, uint64_t dst_bytes, shf_tab_job* jobs,
                                                         const uint16_t* __restrict__ maps, uint32_t n_maps,
@@ -321,7 +335,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         wsum[seg & 1][j][2][wave] = ic;
       }
     }
-    __syncthreads();
+    seg_barrier();
     uint64_t seg_k = 0, seg_m = 0;  // this segment's keep and move bytes so far
     uint32_t seg_c = 0;             // and records (packed: keep low, move high half)
     // 3. each ref's record offset in its image, its list entry, its row entry in both images
@@ -368,7 +382,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     if (t == 0 && (kTabData + done_keep > cap || (moving && kTabData + done_move > cap) ||
                    kTabData + done_keep + done_move > 0xffffffffull))
       bad = 1;
-    __syncthreads();
+    seg_barrier();
     if (bad) break;  // workgroup-uniform; nothing past cap was or will be written
 
     // 4. the data chunks this segment completes (every byte below done_*)
