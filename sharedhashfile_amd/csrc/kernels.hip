@@ -633,21 +633,6 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
       reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
-// span_fetch that defines every piece (zero past the span), so that a loop
-// carrying `reg` does not keep the previous tile's pieces live.
-template <int PIECES>
-__device__ __forceinline__ void span_fetch_all(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-  const uint32_t nb = __builtin_amdgcn_readfirstlane(span16);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
-#pragma unroll
-  for (int q = 0; q < PIECES; ++q)
-    reg[q] = (uint32_t)q * 1024u < nb ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2)
-                                      : u32x4{0u, 0u, 0u, 0u};
-}
-
 // Stage the fetched pieces that hold span bytes (lanes past the span's end
 // write nothing: the window may be exactly the span plus its read slack).
 template <int PIECES>
@@ -995,41 +980,12 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#ifndef SHFHB_PP_SORT
-#define SHFHB_PP_SORT 0  // k_span_pp: lanes take the tile's keys in block-count order (experiment)
-#endif
-
-// Hash the staged tile: lane l hashes key l, or (SHFHB_PP_SORT) the key of
-// rank l by block count, so that finished lanes gather in the low lanes.
 template <int OUT>
 __device__ __forceinline__ void span_hash_tile(const uint32_t* lds, const uint8_t* bytes, const SpanTile<true>& ti,
-                                               uint32_t lane, uint32_t seed, const Sink& sink) {
-#if SHFHB_PP_SORT
-  const uint32_t nbk = ti.valid ? min(ti.len >> 4, (1u << 25) - 1u) : 0u;
-  uint32_t v = (nbk << 6) | lane;
-#pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)j);
-      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-      v = keep_min ? min(v, o) : max(v, o);
-    }
-  }
-  const int src = (int)(v & 63u);
-  const uint64_t start = (uint64_t)(uint32_t)__shfl((int)(uint32_t)ti.start, src) |
-                         ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ti.start >> 32), src) << 32);
-  const uint32_t len = (uint32_t)__shfl((int)ti.len, src);
-  const bool valid = __shfl((int)ti.valid, src) != 0;
-  const uint64_t key = ti.key - lane + (uint32_t)src;
-#else
-  const uint64_t start = ti.start, key = ti.key;
-  const uint32_t len = ti.len;
-  const bool valid = ti.valid;
-#endif
-  if (valid) {
-    const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + start - ti.base);
-    store_result<OUT>(sink, key, hash_lds_u(lds, p, len, seed));
+                                               uint32_t seed, const Sink& sink) {
+  if (ti.valid) {
+    const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
+    store_result<OUT>(sink, ti.key, hash_lds_u(lds, p, ti.len, seed));
   }
 }
 
@@ -1066,86 +1022,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
   if (wave == 0 && staged) {
     span_stage<PIECES>(span_lds, reg, ti.span16, lane);
     wave_lds_fence();
-    span_hash_tile<OUT>(span_lds, bytes, ti, lane, seed, sink);
+    span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
   }
   lds_barrier();  // wave 0 is done with the window (its result stores may still be in flight)
   if (wave == 1 && staged) {
     span_stage<PIECES>(span_lds, reg, ti.span16, lane);
     wave_lds_fence();
-    span_hash_tile<OUT>(span_lds, bytes, ti, lane, seed, sink);
+    span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
   }
   if (has && !staged) span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-}
-
-#ifndef SHFHB_PQ_K
-#define SHFHB_PQ_K 0  // k_span_pq: tiles per wave (0: k_span_pp, one tile per wave)
-#endif
-#ifndef SHFHB_PQ_OFFPF
-#define SHFHB_PQ_OFFPF 0  // k_span_pq: load the next tile's offsets before hashing this one
-#endif
-
-// Relay ping-pong: k_span_pp's two waves and one window, but each wave
-// hashes K tiles in turn (tiles 2j + wave of the workgroup's 2K), fetching its
-// next span into registers right after each hash, while the partner hashes.
-// The window then waits for HBM once per 2K tiles. The hand-overs are
-// LDS-only barriers: a wave's span fetch and result stores stay in flight.
-// One wave's part of k_span_pq (FIRST: wave 0, which hashes first). Written
-// per wave so that a wave's held span is not live across its own hash.
-template <int OUT, int PIECES, int K, bool FIRST>
-__device__ __forceinline__ void span_pq_wave(const uint8_t* bytes, const uint64_t* offsets, uint64_t off_base,
-                                             uint64_t n, uint32_t seed, uint32_t cap, const Sink& sink,
-                                             uint32_t* span_lds, uint32_t lane) {
-  const uint64_t ntiles = (n + 63) / 64;
-  uint64_t t = (uint64_t)blockIdx.x * (2u * K) + (FIRST ? 0u : 1u);
-  SpanRaw raw = span_load<true>(offsets, n, t, lane);
-  bool has = t < ntiles;
-  bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-  SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-  bool staged = has && !bad && ti.span16 <= cap;
-  u32x4 reg[PIECES];
-  span_fetch_all<PIECES>(reg, staged ? ti.base : 0u, staged ? ti.span16 : 0u, lane);
-#if SHFHB_PQ_OFFPF
-  SpanRaw nraw = span_load<true>(offsets, n, t + 2u, lane);
-#endif
-  for (uint32_t j = 0; j < K; ++j) {
-    if (!FIRST) lds_barrier();  // the partner is done with the window
-    if (staged) {
-      span_stage<PIECES>(span_lds, reg, ti.span16, lane);
-      wave_lds_fence();
-      span_hash_tile<OUT>(span_lds, bytes, ti, lane, seed, sink);
-    } else if (has) {  // rare: offsets re-read rather than held across the loop
-      span_tile_from_hbm<OUT>(bytes, off_base, n, span_load<true>(offsets, n, t, lane), lane, seed, sink);
-    }
-    if (j + 1 < K) {  // this wave's next tile, in flight while the partner hashes
-      t += 2u;
-#if SHFHB_PQ_OFFPF
-      raw = nraw;
-      if (j + 2 < K) nraw = span_load<true>(offsets, n, t + 2u, lane);
-#else
-      raw = span_load<true>(offsets, n, t, lane);
-#endif
-      has = t < ntiles;
-      bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-      ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-      staged = has && !bad && ti.span16 <= cap;
-      span_fetch_all<PIECES>(reg, staged ? ti.base : 0u, staged ? ti.span16 : 0u, lane);
-    }
-    if (FIRST || j + 1 < K) lds_barrier();  // hand the window over
-    if (FIRST && j + 1 < K) lds_barrier();  // and wait for it back
-  }
-}
-
-template <int OUT, int PIECES, int K>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_span_pq(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint32_t seed, uint32_t cap, Sink sink) {
-  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  if (__builtin_amdgcn_readfirstlane(wave) == 0)
-    span_pq_wave<OUT, PIECES, K, true>(bytes, offsets, off_base, n, seed, cap, sink, span_lds, lane);
-  else
-    span_pq_wave<OUT, PIECES, K, false>(bytes, offsets, off_base, n, seed, cap, sink, span_lds, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1161,6 +1046,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
 // pairs of waves, taking turns on the window as in k_span_pp (the second
 // pair's spans wait in registers).
 // ---------------------------------------------------------------------------
+#ifndef SHFHB_PS_FLIP
+#define SHFHB_PS_FLIP 1
+#endif
 #ifndef SHFHB_SPAN_PAIRSORT
 #define SHFHB_SPAN_PAIRSORT 0
 #endif
@@ -1241,6 +1129,9 @@ __device__ __forceinline__ void span_ps_wave(const uint8_t* bytes, const uint64_
                        : u32x4{0u, 0u, 0u, 0u};
     }
   }
+  // role 0 takes the shorter 64 keys, role 1 the longer; alternated between
+  // the pairs and between workgroups so that every SIMD gets both kinds
+  const uint32_t role = h ^ (SECOND ? 1u : 0u) ^ (SHFHB_PS_FLIP ? (blockIdx.x & 1u) : 0u);
   uint32_t v = 0;
   if (SECOND) {
     lds_barrier();  // the first pair's exchange
@@ -1256,13 +1147,13 @@ __device__ __forceinline__ void span_ps_wave(const uint8_t* bytes, const uint64_
     const uint32_t len = valid ? (uint32_t)(a1 - a0) : 0u;
     const uint32_t p = valid ? (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + (a0 - off_base) - base) : 0u;
     tbl[my] = p | (len << 16);  // p, len < kPsCap < 2^16
-    v = wave_sort_u32(((len >> 4) << 7) | my, lane, h != 0);
+    v = wave_sort_u32(((len >> 4) << 7) | my, lane, role != 0);
     xch[my] = v;
   }
   lds_barrier();  // this pair's halves staged and sorted
   if (staged) {
     const uint32_t o = xch[64u * (1u - h) + lane];
-    const uint32_t idx = (h == 0 ? min(v, o) : max(v, o)) & 127u;
+    const uint32_t idx = (role == 0 ? min(v, o) : max(v, o)) & 127u;
     const uint32_t e = tbl[idx];
     if (idx < kn) store_result<OUT>(sink, k0 + idx, hash_lds_u(lds, e & 0xffffu, e >> 16, seed));
   } else if (my < kn) {  // a bad key or a span over the window: this lane's own key from HBM
@@ -1356,14 +1247,6 @@ static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* of
   const uint64_t tiles = (n + 63) / 64;
   const uint64_t wgs = (tiles + 1) / 2;
   if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
-#if SHFHB_PQ_K
-  {
-    const uint64_t g = (tiles + 2u * SHFHB_PQ_K - 1) / (2u * SHFHB_PQ_K);
-    hipLaunchKernelGGL((k_span_pq<OUT, kSpanPiecesMax, SHFHB_PQ_K>), dim3((unsigned)g), dim3(128), kSpanAlloc, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
-    return hipGetLastError();
-  }
-#endif
   hipLaunchKernelGGL((k_span_pp<OUT, kSpanPiecesMax>), dim3((unsigned)wgs), dim3(128), kSpanAlloc, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
   return hipGetLastError();
