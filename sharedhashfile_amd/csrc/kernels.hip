@@ -1034,150 +1034,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // ---------------------------------------------------------------------------
-// Pair-sorted span kernel (variable-length keys): a wave's block loop runs to
-// the longest key of its 64, so on U[8,512] B keys lanes idle through half of
-// it. Here two waves share a 128-key tile (one contiguous span, one 40-KiB
-// window) and split its keys by length: each sorts its own 64 block counts
-// (bitonic, in-wave shuffles; ascending in wave 0, descending in wave 1), one
-// exchange of the two sorted halves through LDS leaves the 64 shorter keys in
-// wave 0 and the 64 longer in wave 1 (the bitonic split), and each lane hashes
-// the key it was given. A tile's loops then run to about the median and the
-// maximum block count instead of twice the maximum. A workgroup holds two such
-// pairs of waves, taking turns on the window as in k_span_pp (the second
-// pair's spans wait in registers).
-// ---------------------------------------------------------------------------
-#ifndef SHFHB_PS_FLIP
-#define SHFHB_PS_FLIP 1
-#endif
-#ifndef SHFHB_SPAN_PAIRSORT
-#define SHFHB_SPAN_PAIRSORT 0
-#endif
-constexpr uint32_t kPsAlloc = 40u * 1024u;                      // 4 workgroups per CU
-constexpr uint32_t kPsTblBytes = 128u * 4u;                     // per key: u16 start in the span | u16 length << 16
-constexpr uint32_t kPsXchBytes = 128u * 4u;                     // the sorted halves' exchange
-constexpr uint32_t kPsCap = kPsAlloc - kSpanPad - kPsTblBytes - kPsXchBytes;  // span bytes (39360)
-constexpr int kPsPieces = 20;                                   // 1-KiB pieces fetched per wave (2 x 20 >= kPsCap)
-
-// Bitonic sort of one value per lane across the wave (ascending, or descending).
-__device__ __forceinline__ uint32_t wave_sort_u32(uint32_t v, uint32_t lane, bool desc) {
-#pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)j);
-      const bool keep_min = (((lane & j) == 0) == ((lane & k) == 0)) != desc;
-      v = keep_min ? min(v, o) : max(v, o);
-    }
-  }
-  return v;
-}
-
-// One wave's part of a k_span_ps workgroup. SECOND: a wave of the second pair
-// (its span waits in registers while the first pair hashes). Written per pair
-// so that a held span is not live across the same wave's hash.
-template <int OUT, bool SECOND>
-__device__ __forceinline__ void span_ps_wave(const uint8_t* bytes, const uint64_t* offsets, uint64_t off_base,
-                                             uint64_t n, uint32_t seed, const Sink& sink, uint32_t* lds, uint32_t h,
-                                             uint32_t lane) {
-  uint32_t* tbl = lds + (kPsCap + kSpanPad) / 4u;
-  uint32_t* xch = tbl + 128u;
-  const uint64_t k0 = ((uint64_t)blockIdx.x * 2u + (SECOND ? 1u : 0u)) * 128u;
-  const bool has = k0 < n;
-  const uint32_t kn = has ? (uint32_t)min<uint64_t>(128u, n - k0) : 0u;
-  // this lane's key and the other half's (each wave checks all 128 keys' offsets)
-  const uint32_t my = 64u * h + lane, ot = 64u * (1u - h) + lane;
-  uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-  if (my < kn) {
-    a0 = offsets[k0 + my];
-    a1 = offsets[k0 + my + 1];
-  }
-  if (ot < kn) {
-    b0 = offsets[k0 + ot];
-    b1 = offsets[k0 + ot + 1];
-  }
-  const bool bad = __ballot(var_key_bad(a0, a1) || var_key_bad(b0, b1)) != 0;
-  uint64_t base = 0;
-  uint32_t span16 = 0;
-  if (has && !bad) {
-    // the readlane builtins return a signed int: widen through uint32_t
-    const uint64_t f = h == 0 ? a0 : b0;
-    const uint64_t e = ((kn - 1u) >> 6) == h ? a1 : b1;
-    const uint32_t el = (kn - 1u) & 63u;
-    const uint64_t first = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)f) |
-                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32);
-    const uint64_t end = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)e, el) |
-                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), el) << 32);
-    if (end > first) {
-      const uint64_t b = reinterpret_cast<uintptr_t>(bytes);
-      base = (b + (first - off_base)) & ~(uint64_t)15;
-      const uint64_t span = ((b + (end - off_base) + 15u) & ~(uint64_t)15) - base;
-      span16 = span > 0xffffffffull ? 0xffffffffu : (uint32_t)span;
-    }
-  }
-  const bool staged = has && !bad && span16 <= kPsCap;
-  u32x4 reg[kPsPieces];
-  if (staged) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-    const uint32_t nb = __builtin_amdgcn_readfirstlane(span16);
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
-#pragma unroll
-    for (int q = 0; q < kPsPieces; ++q) {
-      const uint32_t at = (kPsPieces * h + (uint32_t)q) * 1024u;
-      reg[q] = at < nb ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, at + lane * 16u, 0, 2 /* nt */)
-                       : u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  // role 0 takes the shorter 64 keys, role 1 the longer; alternated between
-  // the pairs and between workgroups so that every SIMD gets both kinds
-  const uint32_t role = h ^ (SECOND ? 1u : 0u) ^ (SHFHB_PS_FLIP ? (blockIdx.x & 1u) : 0u);
-  uint32_t v = 0;
-  if (SECOND) {
-    lds_barrier();  // the first pair's exchange
-    lds_barrier();  // the first pair is done with the window
-  }
-  if (staged) {
-#pragma unroll
-    for (int q = 0; q < kPsPieces; ++q) {
-      const uint32_t at = (kPsPieces * h + (uint32_t)q) * 1024u + lane * 16u;
-      if (at < span16) reinterpret_cast<u32x4*>(lds)[at / 16u] = reg[q];
-    }
-    const bool valid = my < kn;
-    const uint32_t len = valid ? (uint32_t)(a1 - a0) : 0u;
-    const uint32_t p = valid ? (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + (a0 - off_base) - base) : 0u;
-    tbl[my] = p | (len << 16);  // p, len < kPsCap < 2^16
-    v = wave_sort_u32(((len >> 4) << 7) | my, lane, role != 0);
-    xch[my] = v;
-  }
-  lds_barrier();  // this pair's halves staged and sorted
-  if (staged) {
-    const uint32_t o = xch[64u * (1u - h) + lane];
-    const uint32_t idx = (role == 0 ? min(v, o) : max(v, o)) & 127u;
-    const uint32_t e = tbl[idx];
-    if (idx < kn) store_result<OUT>(sink, k0 + idx, hash_lds_u(lds, e & 0xffffu, e >> 16, seed));
-  } else if (my < kn) {  // a bad key or a span over the window: this lane's own key from HBM
-    if (var_key_bad(a0, a1)) flag_bad_key(sink);
-    else store_result<OUT>(sink, k0 + my, hash_bytes(bytes + (a0 - off_base), (uint32_t)(a1 - a0), seed));
-  }
-  if (!SECOND) {
-    lds_barrier();  // done with the window
-    lds_barrier();  // (the second pair's exchange)
-  }
-}
-
-template <int OUT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_span_ps(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint32_t seed, Sink sink) {
-  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
-  extern __shared__ __attribute__((aligned(16))) uint32_t ps_lds[];
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (wave < 2) span_ps_wave<OUT, false>(bytes, offsets, off_base, n, seed, sink, ps_lds, wave & 1u, lane);
-  else span_ps_wave<OUT, true>(bytes, offsets, off_base, n, seed, sink, ps_lds, wave & 1u, lane);
-}
-
-// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // Workgroups of `kernel` that fit on the whole device at once (cached per device).
@@ -1252,16 +1108,6 @@ static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* of
   return hipGetLastError();
 }
 
-template <int OUT>
-static hipError_t launch_var_span_pairsort(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                                           uint32_t seed, const Sink& sink, hipStream_t st) {
-  const uint64_t wgs = (n + 255) / 256;  // two 128-key tiles per workgroup
-  if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_span_ps<OUT>, dim3((unsigned)wgs), dim3(256), kPsAlloc, st,
-                     reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, sink);
-  return hipGetLastError();
-}
-
 template <int OUT, int PIECES, bool RFB>
 static hipError_t launch_var_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
                                   uint32_t seed, const Sink& sink, hipStream_t st, uint32_t need) {
@@ -1287,11 +1133,6 @@ static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64
                               uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0) {
   if constexpr (VAR) {
     const double need = key_bytes && n ? 64.0 * (double)key_bytes / (double)n * 1.1 + 512.0 + kSpanPad : 1e30;
-    // 128-key tiles whose spans fit 40 KiB (config D's U[8,512] B keys): pair-sorted
-    if constexpr (OUT != kOutProbe)
-      if (SHFHB_SPAN_PAIRSORT && key_bytes && n && 128.0 * (double)key_bytes / (double)n * 1.1 + 512.0 <= kPsCap &&
-          need > 10240.0 + kSpanPad)
-        return launch_var_span_pairsort<OUT>(bytes, offsets, off_base, n, seed, sink, st);
     // windows over 10 KiB (config D's U[8,512] B keys): two waves per window
     if constexpr (OUT != kOutProbe)
       if (SHFHB_SPAN_PINGPONG && need > 10240.0 + kSpanPad)
