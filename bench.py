@@ -508,7 +508,20 @@ def time_host_inclusive(args, dev):
     lib = hb.load()
     n = args.host_keys
     res = {"unit": "keys/s", "note": "never `value`: PCIe-bound; sample = %d keys per batch, median of the "
-                                     "timed repeats after one untimed call" % n}
+                                     "timed repeats after one untimed call; *_pinned = page-locked caller buffers "
+                                     "(16-B keys: the kernel reads and writes them over PCIe, zero copy), "
+                                     "*_pinned_staged = the same through hipMemcpyAsync both ways" % n}
+
+    def _staged(fn):  # page-locked buffers through the copy-engine pipeline (zero copy off)
+        old = os.environ.get("SHF_HB_ZERO_COPY_MAX_KEY")
+        os.environ["SHF_HB_ZERO_COPY_MAX_KEY"] = "0"
+        try:
+            return fn()
+        finally:
+            if old is None:
+                os.environ.pop("SHF_HB_ZERO_COPY_MAX_KEY", None)
+            else:
+                os.environ["SHF_HB_ZERO_COPY_MAX_KEY"] = old
     keys = device_random_bytes(n * 16, 77, dev).cpu().numpy()
     g = torch.Generator(device=dev)
     g.manual_seed(78)
@@ -529,6 +542,8 @@ def time_host_inclusive(args, dev):
                                                               hb.MEM_HOST), 5),
         ("fixed16_pinned", lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED, po.data_ptr(), hb.MEM_HOST),
          5),
+        ("fixed16_pinned_staged", lambda: _staged(lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED,
+                                                                                   po.data_ptr(), hb.MEM_HOST)), 5),
         ("var_pageable", lambda: lib.shf_hash_batch_var(data.ctypes.data, off.ctypes.data, n, SEED, vout.ctypes.data,
                                                         hb.MEM_HOST), 3),
         ("var_pinned", lambda: lib.shf_hash_batch_var(pd.data_ptr(), poff.data_ptr(), n, SEED, vpo.data_ptr(),

@@ -433,11 +433,53 @@ int host_fixed_big(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n,
   return SHF_HB_OK;
 }
 
+// Zero copy: page-locked caller buffers that the device can address are read
+// and written by the hashing kernel itself over PCIe. The copy engines run one
+// direction at a time (H2D 57 GB/s, D2H 57 GB/s, both at once 28-48 GB/s each,
+// tools/host_zero_copy_probe.py), while a kernel's loads and stores use both
+// directions together. 160 MB of keys, G keys/s zero copy vs staged
+// (profiles/r2/host_zero_copy/): 16 B 2.54 vs 1.74, 32 B 1.55 vs 1.11,
+// 48 B 1.01 vs 0.81, 64 B 0.79 vs 0.68, 128 B 0.38 vs 0.33. Used for keys up
+// to SHF_HB_ZERO_COPY_MAX_KEY bytes (default 128; 0 turns it off): past that
+// the keys dominate the traffic and a kernel's PCIe reads (~49 GB/s at
+// 128 B) approach the copy engine's 57 GB/s.
+uint32_t zero_copy_max_key() {
+  const char* e = getenv("SHF_HB_ZERO_COPY_MAX_KEY");
+  if (!e) return 128u;
+  const long v = strtol(e, nullptr, 10);
+  return v < 0 ? 0u : (uint32_t)std::min<long>(v, 1L << 20);
+}
+
+// Device address of host bytes [p, p + bytes), when they lie in one
+// page-locked allocation that the current device maps; else nullptr.
+void* host_range_device_ptr(const void* p, size_t bytes) {
+  if (!p || !bytes) return nullptr;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  void* d = nullptr;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess ||
+      reinterpret_cast<uintptr_t>(p) + bytes > reinterpret_cast<uintptr_t>(base) + size ||
+      hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
 // Host-memory fixed-length pipeline on the current device.
 int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
+  if (job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
+    void* dk = host_range_device_ptr(keys, (size_t)n * key_len);
+    void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)) : nullptr;
+    if (dh) {
+      HB_TRY(shfhb::launch_fixed(dk, key_len, n, seed, out_sink(dh), shfhb::kOutHash, c->st[0], shfhb::kKernelAuto));
+      HB_TRY(hipStreamSynchronize(c->st[0]));
+      return SHF_HB_OK;
+    }
+  }
   if ((uint64_t)key_len > stage_bytes()) return host_fixed_big(c, keys, key_len, n, seed, job);
   const int ns = pipeline_slots();
   const uint64_t per = key_len ? std::max<uint64_t>(1, stage_bytes() / key_len) : (uint64_t)1 << 22;

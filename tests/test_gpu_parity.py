@@ -448,6 +448,31 @@ def test_host_pinned_buffers(hb, dev, oracle):
     assert np.array_equal(out2.numpy().view(np.uint64), oracle.hash_var(data.numpy(), off.numpy().view(np.uint64)))
 
 
+@pytest.mark.parametrize("key_len", [1, 7, 16, 24, 32, 33])
+def test_host_zero_copy(hb, dev, oracle, monkeypatch, key_len):
+    """Page-locked caller buffers, keys up to SHF_HB_ZERO_COPY_MAX_KEY: the
+    kernel reads keys and writes hashes over PCIe itself. Interior pointers
+    (unaligned keys, an output that starts past the allocation's first record),
+    the staged path forced (0), and a pageable output (staged) give the same
+    bits as the oracle."""
+    lib = hb.load()
+    n = 100_003
+    pad = 5
+    keys = torch.randint(0, 256, (n * key_len + 2 * pad,), dtype=torch.uint8).pin_memory()
+    flat = keys.numpy()[pad:pad + n * key_len]
+    want = oracle.hash_fixed(flat, key_len, threads=8)
+    for env in ("32", "0", "1048576"):
+        monkeypatch.setenv("SHF_HB_ZERO_COPY_MAX_KEY", env)
+        out = torch.zeros((n + 3, 2), dtype=torch.int64).pin_memory()
+        rc = lib.shf_hash_batch_fixed(keys.data_ptr() + pad, key_len, n, 12345, out.data_ptr() + 48, hb.MEM_HOST)
+        assert rc == 0
+        assert np.array_equal(out.numpy().view(np.uint64)[3:], want), env
+        assert not out.numpy()[:3].any()
+    pageable = np.zeros((n, 2), dtype=np.uint64)
+    assert lib.shf_hash_batch_fixed(keys.data_ptr() + pad, key_len, n, 12345, pageable.ctypes.data, hb.MEM_HOST) == 0
+    assert np.array_equal(pageable, want)
+
+
 def test_host_huge_single_key(hb, dev, oracle):
     n_big = (70 << 20) + 9  # one key larger than a staging chunk
     data = np.frombuffer(splitmix_bytes(n_big + 100, 5), dtype=np.uint8)
