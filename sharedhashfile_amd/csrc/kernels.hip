@@ -633,21 +633,6 @@ __device__ __forceinline__ void span_fetch(u32x4 (&reg)[PIECES], uint64_t base, 
       reg[q] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2 /* nt */);
 }
 
-// span_fetch that defines every piece (zero past the span), so that a loop
-// carrying `reg` does not keep the previous tile's pieces live.
-template <int PIECES>
-__device__ __forceinline__ void span_fetch_all(u32x4 (&reg)[PIECES], uint64_t base, uint32_t span16, uint32_t lane) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-  const uint32_t nb = __builtin_amdgcn_readfirstlane(span16);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32)), (short)0, (int)nb, 0x00020000);
-#pragma unroll
-  for (int q = 0; q < PIECES; ++q)
-    reg[q] = (uint32_t)q * 1024u < nb ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)q * 1024u + lane * 16u, 0, 2)
-                                      : u32x4{0u, 0u, 0u, 0u};
-}
-
 // Stage the fetched pieces that hold span bytes (lanes past the span's end
 // write nothing: the window may be exactly the span plus its read slack).
 template <int PIECES>
@@ -1049,97 +1034,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // ---------------------------------------------------------------------------
-// Packed-pool span kernel (experiment): k_span_pp's fixed 20-KiB windows hold
-// a 16.6-KB mean span (config D), so a sixth of the LDS sits idle. Here eight
-// waves share an 80-KiB pool and stage their spans back to back: in each
-// phase every wave posts the bytes its fetched span needs, all waves compute
-// the same first-fit assignment (starting at a rotating wave), the assigned
-// waves stage and hash, and an LDS-only barrier ends the phase; each wave
-// fetches its next tile into registers right after its hash (the next
-// tile's offsets are loaded one tile ahead). Tiles with a bad key or a span
-// over 20 KiB are hashed from HBM outside the pool.
-// ---------------------------------------------------------------------------
-#ifndef SHFHB_SPAN_RING
-#define SHFHB_SPAN_RING 0  // tiles per wave (0: k_span_pp)
-#endif
-constexpr uint32_t kRingWaves = 8;
-constexpr uint32_t kRingAlloc = 80u * 1024u;       // 2 workgroups per CU
-constexpr uint32_t kRingPool = kRingAlloc - 64u;   // then the posted needs, one word per wave
-
-template <int OUT, int K>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_span_ring(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint32_t seed, Sink sink) {
-  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held span: k_span");
-  extern __shared__ __attribute__((aligned(16))) uint32_t ring_lds[];
-  uint32_t* need = ring_lds + kRingPool / 4u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  const uint64_t ntiles = (n + 63) / 64;
-  const uint64_t t0 = (uint64_t)blockIdx.x * (kRingWaves * K) + wave;  // this wave's tiles: t0 + 8j
-  constexpr uint32_t cap = kSpanAlloc - kSpanPad;
-  uint32_t j = 0;  // this wave's next tile to load
-  SpanRaw nraw = span_load<true>(offsets, n, t0, lane);
-  SpanTile<true> ti;
-  bool pending = false;
-  u32x4 reg[kSpanPiecesMax];
-  // load this wave's next stageable tile into registers (tiles that cannot be
-  // staged are hashed from HBM on the way); every piece of `reg` is defined
-  auto next_tile = [&]() {
-    pending = false;
-    uint64_t base = 0;
-    uint32_t span16 = 0;
-    while (j < K) {
-      const uint64_t t = t0 + (uint64_t)kRingWaves * j;
-      if (t >= ntiles) {
-        j = K;
-        break;
-      }
-      const SpanRaw raw = nraw;
-      ++j;
-      if (j < K) nraw = span_load<true>(offsets, n, t0 + (uint64_t)kRingWaves * j, lane);
-      const bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
-      ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
-      if (!bad && ti.span16 <= cap) {
-        pending = true;
-        base = ti.base;
-        span16 = ti.span16;
-        break;
-      }
-      span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
-    }
-    span_fetch_all<kSpanPiecesMax>(reg, base, span16, lane);
-  };
-  next_tile();
-  for (uint32_t phase = 0;; ++phase) {
-    if (lane == 0) need[wave] = pending ? ((ti.span16 + kSpanPad + 15u) & ~15u) : 0u;
-    lds_barrier();
-    uint32_t off = 0, mine = 0xffffffffu;
-    bool any = false;
-#pragma unroll
-    for (uint32_t i = 0; i < kRingWaves; ++i) {
-      const uint32_t w2 = (phase + i) & (kRingWaves - 1u);
-      const uint32_t v = __builtin_amdgcn_readfirstlane(need[w2]);
-      if (v) {
-        any = true;
-        if (off + v <= kRingPool) {
-          if (w2 == wave) mine = off;
-          off += v;
-        }
-      }
-    }
-    if (!any) break;  // workgroup-uniform: every wave read the same needs
-    if (mine != 0xffffffffu) {
-      uint32_t* win = ring_lds + mine / 4u;
-      span_stage<kSpanPiecesMax>(win, reg, ti.span16, lane);
-      wave_lds_fence();
-      span_hash_tile<OUT>(win, bytes, ti, seed, sink);
-      next_tile();
-    }
-    lds_barrier();  // the pool is free; needs may be rewritten
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // Workgroups of `kernel` that fit on the whole device at once (cached per device).
@@ -1209,14 +1103,6 @@ static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* of
   const uint64_t tiles = (n + 63) / 64;
   const uint64_t wgs = (tiles + 1) / 2;
   if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
-#if SHFHB_SPAN_RING
-  {
-    const uint64_t g = (tiles + kRingWaves * SHFHB_SPAN_RING - 1) / (kRingWaves * SHFHB_SPAN_RING);
-    hipLaunchKernelGGL((k_span_ring<OUT, SHFHB_SPAN_RING>), dim3((unsigned)g), dim3(512), kRingAlloc, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, sink);
-    return hipGetLastError();
-  }
-#endif
   hipLaunchKernelGGL((k_span_pp<OUT, kSpanPiecesMax>), dim3((unsigned)wgs), dim3(128), kSpanAlloc, st,
                      reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, seed, kSpanAlloc - kSpanPad, sink);
   return hipGetLastError();
