@@ -145,6 +145,9 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
   *reinterpret_cast<volatile int32_t*>(&job->status) = v;
 }
 
+#ifndef SHFHB_TAB_SPEC_NEXT
+#define SHFHB_TAB_SPEC_NEXT 1
+#endif
 #ifndef SHFHB_TAB_CHUNKS
 #define SHFHB_TAB_CHUNKS 2  // 16-B chunks per lane in flight (2 and 4 within 5 %, 8 slower: profiles/r2/ab_tab)
 #endif
@@ -162,6 +165,9 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
   constexpr uint32_t Q = SHFHB_TAB_CHUNKS;
   for (uint64_t base = c_begin; base < c_end; base += Q * kThreads) {
     unsigned __int128 v[Q];
+#if SHFHB_TAB_SPEC_NEXT
+    unsigned __int128 vn[Q];  // the next record's first 16 B, for a chunk that crosses into it
+#endif
     uint32_t k[Q], lo[Q], hi[Q], st[Q];
     int64_t a[Q];
 #pragma unroll
@@ -180,6 +186,11 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
       if (lo[q] < hi[q]) {
         st[q] = l ? L.end(l - 1) : 0u;
         v[q] = load16(src, src_len, (uint64_t)L.pos(l) + (lo[q] - st[q]));
+#if SHFHB_TAB_SPEC_NEXT
+        // issued beside the first load, so a chunk crossing a record end (about
+        // one in eight) does not wait for a second dependent round trip
+        vn[q] = L.end(l) < hi[q] ? load16(src, src_len, L.pos(l + 1)) : (unsigned __int128)0;
+#endif
       }
     }
 #pragma unroll
@@ -195,7 +206,11 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
         if (b >= hi[q]) break;
         s0 = e;
         ++kk;
+#if SHFHB_TAB_SPEC_NEXT
+        x = kk == k[q] + 1u ? vn[q] : load16(src, src_len, L.pos(kk));
+#else
         x = load16(src, src_len, L.pos(kk));
+#endif
       }
       uint8_t* dst = reinterpret_cast<uint8_t*>((base + q * kThreads + t) << 4);
       const uint32_t o = (uint32_t)((int64_t)lo[q] - a[q]);  // the chunk's first byte it writes
@@ -224,6 +239,26 @@ constexpr uint32_t kSegs = SHFHB_TAB_SEGS;
 constexpr uint32_t kSegRefs = kTabRefs / kSegs;           // 2048
 constexpr uint32_t kSlabs = kSegRefs / kThreads;          // 4: ref = seg * 2048 + slab * 512 + thread
 
+// Phase stamps for profiling builds only (-DSHFHB_TAB_STAMPS=1, read back with
+// shf_tab_debug_stamps): thread 0 of each workgroup records the 100-MHz
+// real-time counter at fixed points, through ordinary vector stores.
+#ifndef SHFHB_TAB_STAMPS
+#define SHFHB_TAB_STAMPS 0
+#endif
+#if SHFHB_TAB_STAMPS
+constexpr uint32_t kStampWgs = 4096, kStamps = 16;
+__device__ uint64_t g_tab_stamps[kStampWgs * kStamps];
+#define TAB_STAMP(k)                                                                              \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < kStampWgs)                                               \
+      g_tab_stamps[blockIdx.x * kStamps + (k)] = __builtin_amdgcn_s_memrealtime();                \
+  } while (0)
+#else
+#define TAB_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 #ifndef SHFHB_TAB_LDS_BARRIER
 #define SHFHB_TAB_LDS_BARRIER 1
 #endif
@@ -246,6 +281,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ uint32_t e_pos[kTabRefs];
   __shared__ uint32_t wsum[2][kSlabs][4][kWaves];  // per segment parity, slab, quantity (keep/move bytes/refs), wave
   __shared__ int bad;
+  TAB_STAMP(0);
   shf_tab_job* job = jobs + blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const uint64_t src_len = job->src_len;
@@ -336,6 +372,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       }
     }
     seg_barrier();
+    TAB_STAMP(1 + 3 * seg);
     uint64_t seg_k = 0, seg_m = 0;  // this segment's keep and move bytes so far
     uint32_t seg_c = 0;             // and records (packed: keep low, move high half)
     // 3. each ref's record offset in its image, its list entry, its row entry in both images
@@ -383,6 +420,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                    kTabData + done_keep + done_move > 0xffffffffull))
       bad = 1;
     seg_barrier();
+    TAB_STAMP(2 + 3 * seg);
     if (bad) break;  // workgroup-uniform; nothing past cap was or will be written
 
     // 4. the data chunks this segment completes (every byte below done_*)
@@ -393,6 +431,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, end_m, move_type, t);
       next_m = end_m;
     }
+    TAB_STAMP(3 + 3 * seg);
   }
   if (bad) {
     if (t == 0) flag(job, SHF_HB_ERR_ARG);
@@ -401,6 +440,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // the last partial chunk of each image
   copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, (d0k + done_keep + 15u) >> 4, keep_type, t);
   if (moving) copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, (d0m + done_move + 15u) >> 4, move_type, t);
+  TAB_STAMP(13);
 
   // 5. headers: tab_size (replayed growth), tab_used, tab_refs_used (SHF_TAB_APPEND and
   //    SHF_TAB_REF_COPY both count each copied ref, shf.c:608, :651), free pos, free, data used
@@ -418,8 +458,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       store_u32(img + 20, (uint32_t)total);
     }
   }
+  TAB_STAMP(14);
   if (t == 0) flag(job, SHF_HB_OK);
 }
+
+#if SHFHB_TAB_STAMPS
+int tab_debug_stamps(uint64_t* out, uint64_t n) {
+  if (n > (uint64_t)kStampWgs * kStamps) n = (uint64_t)kStampWgs * kStamps;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tab_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint64_t dst_bytes, shf_tab_job* jobs,
                             uint32_t n_jobs, const uint16_t* maps, uint32_t n_maps, const shf_tab_params& prm,
@@ -431,3 +479,9 @@ hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint
 }
 
 }  // namespace shfhb
+
+#if SHFHB_TAB_STAMPS
+extern "C" __attribute__((visibility("default"))) int shf_tab_debug_stamps(uint64_t* out, uint64_t n) {
+  return shfhb::tab_debug_stamps(out, n);
+}
+#endif
