@@ -281,6 +281,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ uint32_t e_pos[kTabRefs];
   __shared__ uint32_t wsum[2][kSlabs][4][kWaves];  // per segment parity, slab, quantity (keep/move bytes/refs), wave
   __shared__ int bad;
+  __shared__ uint32_t max_len;  // the longest record copied (either image)
   TAB_STAMP(0);
   shf_tab_job* job = jobs + blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
@@ -293,6 +294,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const uint32_t tab_new = job->tab_new, keep_type = job->keep_type, move_type = job->move_type;
   const uint64_t cap = job->cap;
   if (t == 0) {
+    max_len = 0;
     // every byte a job names lies in its buffer; images are 8-B aligned
     bad = src_len < kTabData || job->src > src_bytes || src_len > src_bytes - job->src || cap < kTabData ||
           job->keep > dst_bytes || cap > dst_bytes - job->keep ||
@@ -356,6 +358,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       to_move |= (uint32_t)(moving && map[w0[j] & 0x7ffu] == tab_new) << j;  // shf.c:765-767
     }
     if (mine_bad) bad = 1;
+    {
+      uint32_t m = max(max(len[0], len[1]), max(len[2], len[3]));
+      static_assert(kSlabs == 4, "max over the slabs");
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+      if (lane == 0) atomicMax(&max_len, m);  // read after the segment loop's barriers
+    }
 
     // 2. scans in ref order (slab by slab, thread by thread): in the wave, then over the waves
     //    through LDS. Per ref: its size in keep, in move, and the keep and move record counts
@@ -446,7 +455,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   //    SHF_TAB_REF_COPY both count each copied ref, shf.c:608, :651), free pos, free, data used
   if (wave == 0 || (moving && wave == 1)) {
     const bool m = wave == 1;
-    const uint64_t size = replay_tab_size(m ? LM : LK, m ? refs_move : refs_keep, factor, lane);
+    // When no record needs more than a page (len x factor <= 4096), each growth
+    // SHF_TAB_APPEND makes is exactly one page (tab sizes are page multiples),
+    // so the size is the first page multiple that holds all the data: no replay.
+    const uint64_t total_m = m ? done_move : done_keep;
+    const uint64_t size = (uint64_t)max_len * factor <= kPage
+                              ? max(mod_page(kTabData), mod_page(kTabData + total_m))
+                              : replay_tab_size(m ? LM : LK, m ? refs_move : refs_keep, factor, lane);
     if (lane == 0) {
       uint8_t* img = m ? move : keep;
       const uint64_t total = m ? done_move : done_keep;

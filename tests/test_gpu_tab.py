@@ -183,3 +183,21 @@ def test_synthetic_tabs_match_oracle(hb, dev, oracle, n_refs, kl, vl, seed):
             assert move is None
         else:
             assert np.array_equal(move, wm)
+
+
+@pytest.mark.parametrize("factor", [1, 8, 20, 40])
+def test_tab_size_growth_factor(hb, dev, oracle, factor):
+    """The images' tab_size: closed form while every record times the growth
+    factor fits a page (each SHF_TAB_APPEND growth is then one page), the
+    growth replay otherwise (records of up to 201 B: factor 40 replays)."""
+    from sharedhashfile_amd.tabgen import synth_tab
+
+    img, m, old = synth_tab(7, n_refs=4500, key_lo=16, key_hi=64, val_lo=8, val_hi=128)
+    new = (old + 77) % 2048
+    m2 = hb.tab_part_redirect(m, old, new)
+    got = hb.tab_copy([img, img], [m2, m2], [new, hb.TAB_NONE], factor=factor, keep_type=0x3E, move_type=0xBE)
+    for (keep, move), tn in zip(got, [new, hb.TAB_NONE]):
+        wk, wm = oracle.tab_split(img, m2, tn, False, 0, 0, factor, cap=keep.size, keep_type=0x3E, move_type=0xBE)
+        assert np.array_equal(keep, wk)
+        if tn != hb.TAB_NONE:
+            assert np.array_equal(move, wm)
