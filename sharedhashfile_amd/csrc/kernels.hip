@@ -723,11 +723,6 @@ __device__ __forceinline__ u32x4 lds_read16(const uint32_t* lds, uint32_t byte) 
   return *(lds_u32x4_a1*)((lds_u8*)lds + byte);  // generic -> LDS address space (lds is an LDS pointer)
 }
 
-#ifndef SHFHB_PP_PRIO
-#define SHFHB_PP_PRIO 0  // k_span_pp: raise a hashing wave's issue priority as it progresses (experiment)
-#endif
-
-template <int PRIO = 0>
 __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
   const uint32_t nblocks = len >> 4;
   State s{seed, seed};
@@ -740,13 +735,6 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
   u32x4 nxt = lds_read16(lds, p + 16u);
   uint64_t m1 = mix_k1(pack64(cur.x, cur.y)), m2 = mix_k2(pack64(cur.z, cur.w));
   for (uint32_t j = 0; j < nblocks; ++j) {
-    if constexpr (PRIO == 1) {  // the further a wave is, the sooner its window should free: priority 1, 2, 3
-      if (j == 8u) __builtin_amdgcn_s_setprio(1);
-      if (j == 16u) __builtin_amdgcn_s_setprio(2);
-      if (j == 24u) __builtin_amdgcn_s_setprio(3);
-    } else if constexpr (PRIO == 2) {
-      if (j == 16u) __builtin_amdgcn_s_setprio(2);
-    }
     const u32x4 nn = lds_read16(lds, p + 16u * j + 32u);
     const uint64_t n1 = mix_k1(pack64(nxt.x, nxt.y)), n2 = mix_k2(pack64(nxt.z, nxt.w));
     chain_block(s, m1, m2);
@@ -997,8 +985,7 @@ __device__ __forceinline__ void span_hash_tile(const uint32_t* lds, const uint8_
                                                uint32_t seed, const Sink& sink) {
   if (ti.valid) {
     const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
-    store_result<OUT>(sink, ti.key, hash_lds_u<(SHFHB_PP_PRIO == 3 ? 0 : SHFHB_PP_PRIO)>(lds, p, ti.len, seed));
-    if (SHFHB_PP_PRIO == 1 || SHFHB_PP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    store_result<OUT>(sink, ti.key, hash_lds_u(lds, p, ti.len, seed));
   }
 }
 
@@ -1021,14 +1008,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint64_t t = 2u * (uint64_t)blockIdx.x + wave;  // this wave's tile (past the last: idle, barriers only)
   const uint64_t ntiles = (n + 63) / 64;
   const bool has = t < ntiles;
-  if (SHFHB_PP_PRIO == 3) __builtin_amdgcn_s_setprio(3);  // issue the offsets and span loads first
   const SpanRaw raw = span_load<true>(offsets, n, t, lane);  // keys past n: o0 = o1 = 0
   const bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
   const SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
   const bool staged = has && !bad && ti.span16 <= cap;
   u32x4 reg[PIECES];
   if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
-  if (SHFHB_PP_PRIO == 3) __builtin_amdgcn_s_setprio(0);
   // Wave 0 stages and hashes; one barrier hands the window to wave 1, which
   // stages and hashes in turn (a wave's own LDS writes and reads are ordered
   // by a wave-level fence). One barrier instead of the four of two
