@@ -38,7 +38,10 @@ constexpr uint32_t kTabHdr = 24;                          // 6 x u32 (shf.privat
 constexpr uint32_t kTabRefs = 512 * 16;                   // SHF_ROWS_PER_TAB x SHF_REFS_PER_ROW
 constexpr uint32_t kTabData = kTabHdr + kTabRefs * 8;     // offsetof(SHF_TAB_MMAP, data) = 65560
 constexpr uint32_t kPage = 4096;                          // SHF_SIZE_PAGE
-constexpr uint32_t kThreads = 512;
+#ifndef SHFHB_TAB_THREADS
+#define SHFHB_TAB_THREADS 512
+#endif
+constexpr uint32_t kThreads = SHFHB_TAB_THREADS;
 constexpr uint32_t kWaves = kThreads / 64;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -359,8 +362,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     if (mine_bad) bad = 1;
     {
-      uint32_t m = max(max(len[0], len[1]), max(len[2], len[3]));
-      static_assert(kSlabs == 4, "max over the slabs");
+      uint32_t m = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kSlabs; ++j) m = max(m, len[j]);
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
       if (lane == 0) atomicMax(&max_len, m);  // read after the segment loop's barriers
