@@ -112,6 +112,29 @@ def main():
     os.environ.pop("SHF_HB_ZERO_COPY_MAX_KEY")
     print("library zero-copy results equal staged: %s" % same, flush=True)
 
+    # pageable caller buffers: staged pipeline vs registering them per call (hipHostRegister) + zero copy
+    import numpy as _np
+    pk_np = _np.ascontiguousarray(keys.numpy())
+    out_np = _np.zeros((n, 2), dtype=_np.uint64)
+    res["pageable_staged"] = n / timeit(lambda: hb._check(lib.shf_hash_batch_fixed(pk_np.ctypes.data, 16, n, seed,
+                                                                                 out_np.ctypes.data, hb.MEM_HOST), "pg"))
+    want = out_np.copy()
+
+    def reg_call():
+        for arr in (pk_np, out_np):
+            rc = hip.hipHostRegister(ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(arr.nbytes), 0)
+            assert rc == 0, rc
+        try:
+            hb._check(lib.shf_hash_batch_fixed(pk_np.ctypes.data, 16, n, seed, out_np.ctypes.data, hb.MEM_HOST), "reg")
+        finally:
+            for arr in (pk_np, out_np):
+                hip.hipHostUnregister(ctypes.c_void_p(arr.ctypes.data))
+
+    out_np[:] = 0
+    res["pageable_register_zero_copy"] = n / timeit(reg_call)
+    same = same and _np.array_equal(out_np, want)
+    print("register+zero-copy results equal staged: %s" % same, flush=True)
+
     dbuf = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     hbuf = torch.empty(n * 16, dtype=torch.uint8).pin_memory()
     nb = n * 16
