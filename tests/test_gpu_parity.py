@@ -448,7 +448,7 @@ def test_host_pinned_buffers(hb, dev, oracle):
     assert np.array_equal(out2.numpy().view(np.uint64), oracle.hash_var(data.numpy(), off.numpy().view(np.uint64)))
 
 
-@pytest.mark.parametrize("key_len", [1, 7, 16, 24, 32, 33])
+@pytest.mark.parametrize("key_len", [1, 7, 16, 24, 32, 33, 128, 129])
 def test_host_zero_copy(hb, dev, oracle, monkeypatch, key_len):
     """Page-locked caller buffers, keys up to SHF_HB_ZERO_COPY_MAX_KEY: the
     kernel reads keys and writes hashes over PCIe itself. Interior pointers
@@ -471,6 +471,9 @@ def test_host_zero_copy(hb, dev, oracle, monkeypatch, key_len):
     pageable = np.zeros((n, 2), dtype=np.uint64)
     assert lib.shf_hash_batch_fixed(keys.data_ptr() + pad, key_len, n, 12345, pageable.ctypes.data, hb.MEM_HOST) == 0
     assert np.array_equal(pageable, want)
+    one = torch.zeros((1, 2), dtype=torch.int64).pin_memory()  # a single key
+    assert lib.shf_hash_batch_fixed(keys.data_ptr() + pad, key_len, 1, 12345, one.data_ptr(), hb.MEM_HOST) == 0
+    assert np.array_equal(one.numpy().view(np.uint64), want[:1])
 
 
 def test_host_huge_single_key(hb, dev, oracle):
