@@ -148,6 +148,9 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
   *reinterpret_cast<volatile int32_t*>(&job->status) = v;
 }
 
+#ifndef SHFHB_TAB_POS_LENGTHS
+#define SHFHB_TAB_POS_LENGTHS 1
+#endif
 #ifndef SHFHB_TAB_SPEC_NEXT
 #define SHFHB_TAB_SPEC_NEXT 1
 #endif
@@ -285,6 +288,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ uint32_t wsum[2][kSlabs][4][kWaves];  // per segment parity, slab, quantity (keep/move bytes/refs), wave
   __shared__ int bad;
   __shared__ uint32_t max_len;  // the longest record copied (either image)
+  __shared__ uint32_t wtot[kWaves];
+  __shared__ int slow;  // packed-tab fast path refused (workgroup-uniform after a barrier)
   TAB_STAMP(0);
   shf_tab_job* job = jobs + blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
@@ -318,10 +323,145 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   uint32_t refs_keep = 0, refs_move = 0;   // records
   uint64_t next_k = d0k >> 4, next_m = d0m >> 4;  // the first chunk not yet copied
 
+  // Packed tabs (variable lengths, tab_data_free == 0: no deleted record, so
+  // the records tile [data, tab_used) in insertion order, shf.c:601-609): a
+  // record's length is the distance from its position to the next record's.
+  // The positions are bucket-sorted in LDS (the record lists' arrays, free
+  // until the segment loop), so no record's two length words are read (a
+  // dependent pair of scattered reads per record). Anything unexpected
+  // (positions outside the data, a shared position, a record under 9 B, a
+  // crowded bucket) falls back to reading the length words.
+  uint32_t lenreg[kSegs * kSlabs / 2];  // two u16 record lengths per word (longer records: no fast path)
+  bool fast = false;
+#if SHFHB_TAB_POS_LENGTHS
+  if (!prm.fixed) {
+    const uint32_t tab_used = load_u32(src + 4), data_free = load_u32(src + 16);  // shf.private.h:59-65
+    if (data_free == 0 && tab_used >= kTabData && tab_used <= src_len && tab_used - kTabData < (1u << 30)) {
+      constexpr uint32_t kBuckets = 4096, kPer = kBuckets / kThreads;
+      uint32_t* pos_by_ref = e_end;   // then each ref's record length
+      uint32_t* counts = e_pos;       // bucket counts, then starts
+      uint16_t* sorted = reinterpret_cast<uint16_t*>(e_pos + kBuckets);  // refs in position order
+      const uint32_t w = (tab_used - kTabData) / kBuckets + 1u;  // bucket width in bytes
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) counts[t * kPer + i] = 0;
+      if (t == 0) slow = 0;
+      seg_barrier();
+      uint32_t pk[kSegs * kSlabs], slot[kSegs * kSlabs];
+#pragma unroll
+      for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
+        const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
+        pk[k] = *reinterpret_cast<const uint32_t*>(src + kTabHdr + 8u * r + 4u);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
+        const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
+        slot[k] = 0;
+        if (pk[k] == 0) continue;
+        if (pk[k] < kTabData || pk[k] >= tab_used) {
+          slow = 1;
+          pk[k] = 0;
+          continue;
+        }
+        pos_by_ref[r] = pk[k];
+        slot[k] = atomicAdd(&counts[(pk[k] - kTabData) / w], 1u);
+      }
+      seg_barrier();
+      // exclusive scan of the bucket counts (thread t: buckets [t * kPer, t * kPer + kPer))
+      uint32_t c[kPer], sum = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) {
+        c[i] = counts[t * kPer + i];
+        sum += c[i];
+        if (c[i] > 64u) slow = 1;  // insertion sort below stays short
+      }
+      const uint32_t incl = wave_incl_scan(sum, lane);
+      if (lane == 63) wtot[wave] = incl;
+      seg_barrier();
+      uint32_t before = 0, n_used = 0;
+#pragma unroll
+      for (uint32_t v = 0; v < kWaves; ++v) {
+        before += v < wave ? wtot[v] : 0u;
+        n_used += wtot[v];
+      }
+      uint32_t at = before + incl - sum;
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) {
+        counts[t * kPer + i] = at;
+        at += c[i];
+      }
+      seg_barrier();
+#pragma unroll
+      for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
+        const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
+        if (pk[k]) sorted[counts[(pk[k] - kTabData) / w] + slot[k]] = (uint16_t)r;
+      }
+      seg_barrier();
+      if (!slow) {  // order each bucket by position (a few entries each)
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+          const uint32_t b0 = counts[t * kPer + i];
+          for (uint32_t x = 1; x < c[i]; ++x) {
+            const uint16_t rx = sorted[b0 + x];
+            const uint32_t px = pos_by_ref[rx];
+            uint32_t y = x;
+            while (y > 0 && pos_by_ref[sorted[b0 + y - 1]] > px) {
+              sorted[b0 + y] = sorted[b0 + y - 1];
+              --y;
+            }
+            sorted[b0 + y] = rx;
+          }
+        }
+      }
+      seg_barrier();
+      uint32_t lens[kSegs * kSlabs];
+      if (!slow) {
+#pragma unroll
+        for (uint32_t m = 0; m < kSegs * kSlabs; ++m) {
+          const uint32_t i = t + m * kThreads;
+          lens[m] = 0;
+          if (i < n_used) {
+            const uint32_t p0 = pos_by_ref[sorted[i]];
+            const uint32_t nx = i + 1 < n_used ? pos_by_ref[sorted[i + 1]] : tab_used;
+            lens[m] = nx - p0;
+            if (lens[m] < 9u || lens[m] > 0xffffu || (i == 0 && p0 != kTabData)) slow = 1;
+          }
+        }
+      }
+      seg_barrier();
+      fast = !slow;
+      if (fast) {
+#pragma unroll
+        for (uint32_t m = 0; m < kSegs * kSlabs; ++m) {
+          const uint32_t i = t + m * kThreads;
+          if (i < n_used) pos_by_ref[sorted[i]] = lens[m];  // now each ref's record length
+        }
+      }
+      seg_barrier();
+      if (fast) {
+#pragma unroll
+        for (uint32_t k = 0; k < kSegs * kSlabs; k += 2) {
+          const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
+          const uint32_t r1 = ((k + 1) / kSlabs) * kSegRefs + ((k + 1) % kSlabs) * kThreads + t;
+          lenreg[k / 2] = (pk[k] ? pos_by_ref[r] : 0u) | ((pk[k + 1] ? pos_by_ref[r1] : 0u) << 16);
+        }
+      }
+      // (the segment loop's first barrier orders these reads before the lists reuse the arrays)
+    }
+  }
+#endif
+
   for (uint32_t seg = 0; seg < kSegs; ++seg) {
     // 1. this thread's refs {tab:11 | rnd:21, pos} (shf.private.h:48-52) and their record lengths
     uint32_t w0[kSlabs], pos[kSlabs], len[kSlabs], kl[kSlabs];
     bool mine_bad = false;
+    uint32_t lseg[kSlabs];  // this segment's lengths from positions (constant indices: registers, not scratch)
+#pragma unroll
+    for (uint32_t j = 0; j < kSlabs; ++j) {
+      uint32_t v = lenreg[j / 2];
+#pragma unroll
+      for (uint32_t g = 1; g < kSegs; ++g) v = seg == g ? lenreg[(g * kSlabs + j) / 2] : v;
+      lseg[j] = (j & 1u) ? v >> 16 : v & 0xffffu;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       const uint32_t r = seg * kSegRefs + j * kThreads + t;
@@ -335,7 +475,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       kl[j] = prm.fixed_key_len;
       if (!prm.fixed && pos[j] != 0) {
         if (pos[j] < kTabData || (uint64_t)pos[j] + 9u > src_len) mine_bad = true;
-        else kl[j] = load_u32(src + pos[j] + 1);
+        else if (!fast) kl[j] = load_u32(src + pos[j] + 1);
       }
     }
     uint32_t to_move = 0;  // bit j: ref of slab j goes to the move image
@@ -346,13 +486,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       const uint64_t p = pos[j];
       uint32_t vl = prm.fixed_val_len;
       if (!prm.fixed) {
-        if (p < kTabData || p + 9u + kl[j] > src_len) {
+        if (p < kTabData || (!fast && p + 9u + kl[j] > src_len)) {
           mine_bad = true;
           continue;
         }
-        vl = load_u32(src + p + 5 + kl[j]);
+        if (!fast) vl = load_u32(src + p + 5 + kl[j]);
       }
-      const uint64_t l = 1ull + len_len + kl[j] + len_len + vl;
+      const uint64_t l = fast ? (uint64_t)lseg[j] : 1ull + len_len + kl[j] + len_len + vl;
       if (p < kTabData || p + l > src_len || l > 0xffffffffull) {
         mine_bad = true;
         continue;

@@ -201,3 +201,40 @@ def test_tab_size_growth_factor(hb, dev, oracle, factor):
         assert np.array_equal(keep, wk)
         if tn != hb.TAB_NONE:
             assert np.array_equal(move, wm)
+
+
+@pytest.mark.parametrize("case", ["packed", "deleted", "shared_pos", "first_gap"])
+def test_lengths_from_positions_and_fallback(hb, dev, oracle, case):
+    """Packed tabs (tab_data_free == 0) take each record's length from the
+    next record's position; a deleted record (tab_data_free > 0), two refs
+    sharing a position, or data not starting at the first record fall back to
+    the length words. Every case against the oracle, which reads the words."""
+    from sharedhashfile_amd.tabgen import TAB_DATA, TAB_HDR, synth_tab
+
+    img, m, old = synth_tab(11, n_refs=3000, key_lo=8, key_hi=80, val_lo=0, val_hi=200)
+    img = img.copy()
+    rows = img[TAB_HDR:TAB_DATA].view(np.uint32).reshape(-1, 2)
+    hdr = img[:TAB_HDR].view(np.uint32)
+    used = np.nonzero(rows[:, 1])[0]
+    if case == "deleted":  # the reference's delete: type byte, ref cleared, free bytes counted (shf.c:612-631)
+        r = used[len(used) // 2]
+        p = int(rows[r, 1])
+        kl = int(img[p + 1:p + 5].view(np.uint32)[0])
+        vl = int(img[p + 5 + kl:p + 9 + kl].view(np.uint32)[0])
+        img[p] = 0x80
+        rows[r, 1] = 0
+        hdr[4] += 1 + 4 + kl + 4 + vl
+        hdr[5] -= 1 + 4 + kl + 4 + vl
+    elif case == "shared_pos":
+        rows[used[7], 1] = rows[used[3], 1]
+    elif case == "first_gap":  # the record at the start of the data is not referenced
+        first = int(np.argmin(np.where(rows[:, 1] > 0, rows[:, 1], 0xffffffff)))
+        rows[first, 1] = 0
+    new = (old + 300) % 2048
+    m2 = hb.tab_part_redirect(m, old, new)
+    got = hb.tab_copy([img, img], [m2, m2], [new, hb.TAB_NONE], keep_type=0x3E, move_type=0xBE)
+    for (keep, move), tn in zip(got, [new, hb.TAB_NONE]):
+        wk, wm = oracle.tab_split(img, m2, tn, cap=keep.size, keep_type=0x3E, move_type=0xBE)
+        assert np.array_equal(keep, wk), case
+        if tn != hb.TAB_NONE:
+            assert np.array_equal(move, wm), case
