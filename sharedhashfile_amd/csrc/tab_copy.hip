@@ -80,14 +80,31 @@ __device__ __forceinline__ void store_partial(uint8_t* p, u32x4 v, uint32_t n) {
   if (n & 1) p[o] = (uint8_t)lo;
 }
 
-// Wave-wide inclusive scan of a u32.
+#ifndef SHFHB_TAB_DPP_SCAN
+#define SHFHB_TAB_DPP_SCAN 1
+#endif
+
+// Wave-wide inclusive scan of a u32 (DPP variant: shifts by 1, 2, 4, 8 lanes
+// within each row of 16, then rows 0 and 1's last lanes added into the rows
+// after them; six VALU adds, no ds_bpermute).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#if SHFHB_TAB_DPP_SCAN
+  (void)lane;
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+  return v;
+#else
 #pragma unroll
   for (uint32_t d = 1; d < 64; d <<= 1) {
     const uint32_t u = (uint32_t)__shfl_up((int)v, d);
     if (lane >= d) v += u;
   }
   return v;
+#endif
 }
 
 // One image's records in image order, in LDS: rank r at e[base + dir * r] (the
