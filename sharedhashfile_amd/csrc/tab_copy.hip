@@ -171,6 +171,9 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
 #ifndef SHFHB_TAB_SPEC_NEXT
 #define SHFHB_TAB_SPEC_NEXT 1
 #endif
+#ifndef SHFHB_TAB_EARLY_MOVE
+#define SHFHB_TAB_EARLY_MOVE 1
+#endif
 #ifndef SHFHB_TAB_CHUNKS
 #define SHFHB_TAB_CHUNKS 2  // 16-B chunks per lane in flight (2 and 4 within 5 %, 8 slower: profiles/r2/ab_tab)
 #endif
@@ -349,6 +352,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // (positions outside the data, a shared position, a record under 9 B, a
   // crowded bucket) falls back to reading the length words.
   uint32_t lenreg[kSegs * kSlabs / 2];  // two u16 record lengths per word (longer records: no fast path)
+  uint32_t mv_all = 0;                   // fast path, early move: bit seg * kSlabs + j = that ref moves
   bool fast = false;
 #if SHFHB_TAB_POS_LENGTHS
   if (!prm.fixed) {
@@ -364,11 +368,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       if (t == 0) slow = 0;
       seg_barrier();
       uint32_t pk[kSegs * kSlabs], slot[kSegs * kSlabs];
+#if SHFHB_TAB_EARLY_MOVE
+      uint32_t wk[kSegs * kSlabs];
+#pragma unroll
+      for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
+        const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
+        const uint2 ref = *reinterpret_cast<const uint2*>(src + kTabHdr + 8u * r);
+        wk[k] = ref.x;
+        pk[k] = ref.y;
+      }
+      // every ref's destination image now (shf.c:765-767), so the segment
+      // loop's scans wait on no global read
+      if (moving) {
+#pragma unroll
+        for (uint32_t k = 0; k < kSegs * kSlabs; ++k)
+          mv_all |= (uint32_t)(pk[k] != 0 && map[wk[k] & 0x7ffu] == tab_new) << k;
+      }
+#else
 #pragma unroll
       for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
         const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
         pk[k] = *reinterpret_cast<const uint32_t*>(src + kTabHdr + 8u * r + 4u);
       }
+#endif
 #pragma unroll
       for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
         const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
@@ -490,12 +512,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       kl[j] = prm.fixed_key_len;
+      if (SHFHB_TAB_EARLY_MOVE && fast) continue;  // positions checked by the fast path's sort
       if (!prm.fixed && pos[j] != 0) {
         if (pos[j] < kTabData || (uint64_t)pos[j] + 9u > src_len) mine_bad = true;
         else if (!fast) kl[j] = load_u32(src + pos[j] + 1);
       }
     }
     uint32_t to_move = 0;  // bit j: ref of slab j goes to the move image
+#if SHFHB_TAB_EARLY_MOVE
+    if (fast) {  // lengths and images known; the refs just loaded are first needed by step 3
+#pragma unroll
+      for (uint32_t j = 0; j < kSlabs; ++j) len[j] = lseg[j];
+      to_move = (mv_all >> (seg * kSlabs)) & ((1u << kSlabs) - 1u);
+    } else
+#endif
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       len[j] = 0;
