@@ -178,6 +178,22 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
 #define SHFHB_TAB_CHUNKS 2  // 16-B chunks per lane in flight (2 and 4 within 5 %, 8 slower: profiles/r2/ab_tab)
 #endif
 
+// The first of L's n records whose end lies past x (n if none), x
+// wave-uniform: a 64-ary search, each round every lane probes one end and a
+// ballot narrows the range 64-fold (8192 records: 3 rounds of one LDS read).
+__device__ __forceinline__ uint32_t wave_first_end_past(const RecList& L, uint32_t n, uint32_t x, uint32_t lane) {
+  uint32_t lo = 0, span = n;  // the answer lies in [lo, lo + span]
+  while (span > 0) {
+    const uint32_t step = (span + 63u) >> 6, hi = lo + span;
+    const uint32_t p = lo + step * (lane + 1u) - 1u;
+    const uint64_t m = __ballot(p >= hi || L.end(p) > x);
+    const uint32_t f = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+    lo = __builtin_amdgcn_readfirstlane(min(lo + step * f, hi));
+    span = __builtin_amdgcn_readfirstlane(min(step - 1u, hi - lo));
+  }
+  return lo;
+}
+
 // Copy the image's data chunks [c_begin, c_end) (absolute 16-B chunks; the
 // image's data starts at absolute byte d0 and its records [0, nrec) are in L,
 // `total` bytes of them): consecutive chunks on consecutive lanes of the
@@ -186,8 +202,16 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
 // ones where it crosses a record end; a record's first byte is its
 // SHF_DATA_TYPE, written as the job says (shf.c:593-596). Only the data's
 // bytes are written (a chunk straddling its start or end is stored partially).
+//
+// A chunk's record: each wave holds 64 consecutive chunks, so one 64-ary
+// search finds the record of its first chunk (r0), every lane loads the end
+// of record r0 + lane and counts it into the histogram `hist` (this wave's 64
+// words of LDS) at the first chunk lane that reaches it; the inclusive scan
+// of the histogram is then each chunk's record - r0 (a chunk 64 or more
+// records on, from records under 16 B, falls back to a binary search).
 __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList& L, uint32_t nrec, uint64_t total,
-                            uint64_t d0, uint64_t c_begin, uint64_t c_end, uint32_t type, uint32_t t) {
+                            uint64_t d0, uint64_t c_begin, uint64_t c_end, uint32_t type, uint32_t t,
+                            uint32_t* hist) {
   constexpr uint32_t Q = SHFHB_TAB_CHUNKS;
   for (uint64_t base = c_begin; base < c_end; base += Q * kThreads) {
     unsigned __int128 v[Q];
@@ -202,7 +226,24 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
       a[q] = (int64_t)(c << 4) - (int64_t)d0;  // the chunk's first byte in the image's data
       lo[q] = a[q] < 0 ? 0u : (uint32_t)a[q];
       hi[q] = c < c_end ? (uint32_t)min<int64_t>(a[q] + 16, (int64_t)total) : lo[q];
-      uint32_t l = 0, h = nrec;  // first record ending past lo
+      uint32_t l = 0, h = nrec;  // first record ending past lo: in [l, h)
+      if (__ballot(lo[q] < hi[q])) {  // lane 0 holds the wave's first chunk, active if any is
+        const uint32_t lane = t & 63u;
+        const uint32_t r0 = wave_first_end_past(L, nrec, __builtin_amdgcn_readfirstlane(lo[q]), lane);
+        const uint32_t e = r0 + lane < nrec ? L.end(r0 + lane) : 0xffffffffu;
+        hist[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        // e > lane 0's lo, so the first chunk lane whose lo reaches e is >= 1
+        const int64_t a0 = a[q] - 16 * (int64_t)lane;
+        const int64_t first = ((int64_t)e - a0 + 15) >> 4;
+        if (e != 0xffffffffu && first < 64) atomicAdd(&hist[(uint32_t)first], 1u);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t cnt = wave_incl_scan(hist[lane], lane);
+        __builtin_amdgcn_wave_barrier();
+        if (cnt < 64u) l = h = r0 + cnt;
+        else l = r0 + 64u;
+      }
+      if (lo[q] >= hi[q]) h = l;  // nothing to copy: no search
       while (l < h) {
         const uint32_t mid = (l + h) >> 1;
         if (L.end(mid) > lo[q]) h = mid;
@@ -310,6 +351,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ uint32_t max_len;  // the longest record copied (either image)
   __shared__ uint32_t wtot[kWaves];
   __shared__ int slow;  // packed-tab fast path refused (workgroup-uniform after a barrier)
+  __shared__ uint32_t whist[kWaves][64];  // copy_chunks' per-wave chunk histograms
   TAB_STAMP(0);
   shf_tab_job* job = jobs + blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
@@ -625,10 +667,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 
     // 4. the data chunks this segment completes (every byte below done_*)
     const uint64_t end_k = (d0k + done_keep) >> 4, end_m = (d0m + done_move) >> 4;
-    copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, end_k, keep_type, t);
+    copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, end_k, keep_type, t, whist[wave]);
     next_k = end_k;
     if (moving) {
-      copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, end_m, move_type, t);
+      copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, end_m, move_type, t, whist[wave]);
       next_m = end_m;
     }
     TAB_STAMP(3 + 3 * seg);
@@ -638,8 +680,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     return;
   }
   // the last partial chunk of each image
-  copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, (d0k + done_keep + 15u) >> 4, keep_type, t);
-  if (moving) copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, (d0m + done_move + 15u) >> 4, move_type, t);
+  copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, (d0k + done_keep + 15u) >> 4, keep_type, t, whist[wave]);
+  if (moving) copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, (d0m + done_move + 15u) >> 4, move_type, t, whist[wave]);
   TAB_STAMP(13);
 
   // 5. headers: tab_size (replayed growth), tab_used, tab_refs_used (SHF_TAB_APPEND and
