@@ -168,9 +168,6 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
 #ifndef SHFHB_TAB_POS_LENGTHS
 #define SHFHB_TAB_POS_LENGTHS 1
 #endif
-#ifndef SHFHB_TAB_SPEC_NEXT
-#define SHFHB_TAB_SPEC_NEXT 1
-#endif
 #ifndef SHFHB_TAB_EARLY_MOVE
 #define SHFHB_TAB_EARLY_MOVE 1
 #endif
@@ -194,6 +191,23 @@ __device__ __forceinline__ uint32_t wave_first_end_past(const RecList& L, uint32
   return lo;
 }
 
+// out with its bytes from sp on taken from x, byte sp replaced by type (a
+// record starting there: its SHF_DATA_TYPE).
+__device__ __forceinline__ unsigned __int128 put_at(unsigned __int128 out, unsigned __int128 x, uint32_t sp,
+                                                   uint32_t type) {
+  const uint32_t sh = 8u * (sp & 7u);
+  const uint64_t ones = ~0ull << sh, eq = 0xffull << sh, tv = (uint64_t)type << sh;
+  uint64_t ol = (uint64_t)out, oh = (uint64_t)(out >> 64);
+  const uint64_t xl = (uint64_t)x, xh = (uint64_t)(x >> 64);
+  if (sp < 8u) {
+    ol = (ol & ~ones) | (xl & ones & ~eq) | tv;
+    oh = xh;
+  } else {
+    oh = (oh & ~ones) | (xh & ones & ~eq) | tv;
+  }
+  return ((unsigned __int128)oh << 64) | ol;
+}
+
 // Copy the image's data chunks [c_begin, c_end) (absolute 16-B chunks; the
 // image's data starts at absolute byte d0 and its records [0, nrec) are in L,
 // `total` bytes of them): consecutive chunks on consecutive lanes of the
@@ -215,9 +229,7 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
   constexpr uint32_t Q = SHFHB_TAB_CHUNKS;
   for (uint64_t base = c_begin; base < c_end; base += Q * kThreads) {
     unsigned __int128 v[Q];
-#if SHFHB_TAB_SPEC_NEXT
-    unsigned __int128 vn[Q];  // the next record's first 16 B, for a chunk that crosses into it
-#endif
+    unsigned __int128 vn[Q];  // the next record's first bytes, for a chunk that crosses into it
     uint32_t k[Q], lo[Q], hi[Q], st[Q];
     int64_t a[Q];
 #pragma unroll
@@ -252,42 +264,34 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
       k[q] = l;
       if (lo[q] < hi[q]) {
         st[q] = l ? L.end(l - 1) : 0u;
-        v[q] = load16(src, src_len, (uint64_t)L.pos(l) + (lo[q] - st[q]));
-#if SHFHB_TAB_SPEC_NEXT
-        // issued beside the first load, so a chunk crossing a record end (about
-        // one in eight) does not wait for a second dependent round trip
-        vn[q] = L.end(l) < hi[q] ? load16(src, src_len, L.pos(l + 1)) : (unsigned __int128)0;
-#endif
+        // loaded so that byte i of each value is the chunk's byte i (the bytes
+        // before a record, or before the image's data, are never stored)
+        const uint32_t e = L.end(l);
+        v[q] = load16(src, src_len, (uint64_t)((int64_t)L.pos(l) + a[q] - (int64_t)st[q]));
+        vn[q] = e < hi[q] ? load16(src, src_len, (uint64_t)((int64_t)L.pos(l + 1) + a[q] - (int64_t)e))
+                          : (unsigned __int128)0;
       }
     }
 #pragma unroll
     for (uint32_t q = 0; q < Q; ++q) {
       if (lo[q] >= hi[q]) continue;
-      unsigned __int128 out = 0, x = v[q];
-      uint32_t b = lo[q], s0 = st[q], kk = k[q];
-      for (;;) {
-        const uint32_t e = L.end(kk), take = min(e, hi[q]) - b, o = (uint32_t)((int64_t)b - a[q]);
-        if (b == s0) x = (x & ~(unsigned __int128)0xff) | type;
-        out |= (x & low_bytes128(take)) << (8 * o);
-        b += take;
-        if (b >= hi[q]) break;
-        s0 = e;
-        ++kk;
-#if SHFHB_TAB_SPEC_NEXT
-        x = kk == k[q] + 1u ? vn[q] : load16(src, src_len, L.pos(kk));
-#else
-        x = load16(src, src_len, L.pos(kk));
-#endif
+      const uint32_t s0 = (uint32_t)((int64_t)lo[q] - a[q]);
+      unsigned __int128 out = v[q], x = vn[q];
+      if (st[q] == lo[q]) out = put_at(out, out, s0, type);  // the record starts at the chunk's first byte
+      for (uint32_t kk = k[q], b = L.end(kk); b < hi[q];) {  // record kk + 1 starts at chunk byte b - a
+        out = put_at(out, x, (uint32_t)((int64_t)b - a[q]), type);
+        const uint32_t e = L.end(++kk);
+        if (e < hi[q]) x = load16(src, src_len, (uint64_t)((int64_t)L.pos(kk + 1) + a[q] - (int64_t)e));
+        b = e;
       }
       uint8_t* dst = reinterpret_cast<uint8_t*>((base + q * kThreads + t) << 4);
-      const uint32_t o = (uint32_t)((int64_t)lo[q] - a[q]);  // the chunk's first byte it writes
-      const uint32_t n = hi[q] - lo[q];
+      const uint32_t n = hi[q] - lo[q];  // bytes written, from chunk byte s0
       if (n == 16u) {
         *reinterpret_cast<u32x4*>(dst) =
             u32x4{(uint32_t)out, (uint32_t)(out >> 32), (uint32_t)(out >> 64), (uint32_t)(out >> 96)};
       } else {
-        const unsigned __int128 y = out >> (8 * o);
-        store_partial(dst + o, u32x4{(uint32_t)y, (uint32_t)(y >> 32), (uint32_t)(y >> 64), (uint32_t)(y >> 96)}, n);
+        const unsigned __int128 y = out >> (8 * s0);
+        store_partial(dst + s0, u32x4{(uint32_t)y, (uint32_t)(y >> 32), (uint32_t)(y >> 64), (uint32_t)(y >> 96)}, n);
       }
     }
   }
