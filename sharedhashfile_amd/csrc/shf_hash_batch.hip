@@ -345,6 +345,7 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 // What a host pipeline writes: hashes and/or row pre-probe records.
 struct HostJob {
   shf_hash128* hash = nullptr;
+  shf_hash128* hash_dev = nullptr;  // device address of `hash` (page-locked): the kernel stores there
   shf_probe* probe = nullptr;
   const shf_row_index* index = nullptr;  // with probe
 };
@@ -366,8 +367,8 @@ int drain_slot(DevCtx* c, int s, Pending& p) {
   return SHF_HB_OK;
 }
 
-// Kernel output of slot s for `job`.
-void job_sink(DevCtx* c, int s, const HostJob& job, shfhb::Sink* k, int* mode) {
+// Kernel output of slot s for `job`, chunk [i0, ...).
+void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k, int* mode) {
   *k = shfhb::Sink();
   if (job.probe) {
     k->out = c->d_probe[s];
@@ -377,7 +378,7 @@ void job_sink(DevCtx* c, int s, const HostJob& job, shfhb::Sink* k, int* mode) {
     k->n_slots = job.index->n_slots;
     *mode = shfhb::kOutProbe;
   } else {
-    k->out = c->d_out[s];
+    k->out = job.hash_dev ? job.hash_dev + i0 : c->d_out[s];
     *mode = shfhb::kOutHash;
   }
 }
@@ -387,7 +388,7 @@ void job_sink(DevCtx* c, int s, const HostJob& job, shfhb::Sink* k, int* mode) {
 int job_d2h(DevCtx* c, int s, const HostJob& job, uint64_t i0, uint64_t cnt, bool hash_pinned, bool probe_pinned,
             Pending* p) {
   *p = Pending{true, nullptr, nullptr, cnt};
-  if (job.hash) {
+  if (job.hash && !job.hash_dev) {
     HB_TRY(hipMemcpyAsync(hash_pinned ? job.hash + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
                           hipMemcpyDeviceToHost, c->st[s]));
     if (!hash_pinned) p->hash = job.hash + i0;
@@ -425,7 +426,7 @@ int host_fixed_big(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n,
     HB_TRY(hipMemcpyAsync(tmp.p, keys + i * (uint64_t)key_len, key_len, hipMemcpyHostToDevice, c->st[0]));
     shfhb::Sink k;
     int mode = 0;
-    job_sink(c, 0, job, &k, &mode);
+    job_sink(c, 0, job, i, &k, &mode);
     HB_TRY(shfhb::launch_fixed(tmp.p, key_len, 1, seed, k, mode, c->st[0], shfhb::kKernelAuto));
     if ((rc = job_d2h(c, 0, job, i, 1, hash_pinned, probe_pinned, &p))) return rc;
     if ((rc = drain_slot(c, 0, p))) return rc;
@@ -466,8 +467,21 @@ void* host_range_device_ptr(const void* p, size_t bytes) {
   return d;
 }
 
+// Staged pipelines with a page-locked hash output: the kernel stores each
+// chunk's hashes straight into it over PCIe (posted writes beside the copy
+// engine's H2D of the next chunk) instead of a D2H copy on the same engine.
+// SHF_HB_DIRECT_OUT=0 turns it off.
+HostJob with_direct_out(const HostJob& job, uint64_t n) {
+  HostJob j = job;
+  const char* e = getenv("SHF_HB_DIRECT_OUT");
+  if (job.hash && !job.probe && !(e && e[0] == '0'))
+    j.hash_dev = static_cast<shf_hash128*>(host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)));
+  return j;
+}
+
 // Host-memory fixed-length pipeline on the current device.
-int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
+int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in) {
+  const HostJob job = with_direct_out(job_in, n);
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -500,7 +514,7 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], src, nb, hipMemcpyHostToDevice, c->st[s]));
     shfhb::Sink k;
     int mode = 0;
-    job_sink(c, s, job, &k, &mode);
+    job_sink(c, s, job, i0, &k, &mode);
     HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto));
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
   }
@@ -511,7 +525,8 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
 
 // Host-memory variable-length pipeline: chunks of whole keys up to stage_bytes()
 // of key bytes (a single larger key gets a chunk of its own).
-int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job) {
+int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job_in) {
+  const HostJob job = with_direct_out(job_in, n);
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -570,7 +585,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
     shfhb::Sink k;
     int mode = 0;
-    job_sink(c, s, job, &k, &mode);
+    job_sink(c, s, job, i0, &k, &mode);
     // the chunk's byte count sizes the span kernel's window (kernels.hip span_window)
     HB_TRY(shfhb::launch_var(d_in, c->d_off[s], base, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto, nb));
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;

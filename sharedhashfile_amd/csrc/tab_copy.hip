@@ -157,10 +157,6 @@ __device__ __forceinline__ unsigned __int128 load16(const uint8_t* src, uint64_t
   return r;
 }
 
-__device__ __forceinline__ unsigned __int128 low_bytes128(uint32_t n) {  // n in [0, 16]
-  return n >= 16u ? ~(unsigned __int128)0 : (((unsigned __int128)1 << (8 * n)) - 1);
-}
-
 __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
   *reinterpret_cast<volatile int32_t*>(&job->status) = v;
 }

@@ -427,8 +427,12 @@ def test_host_pipeline_shapes(hb, dev, oracle, monkeypatch, stage_mb, slots):
     assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
 
 
-def test_host_pinned_buffers(hb, dev, oracle):
-    """Caller buffers already page-locked: DMA'd directly (no staging copy)."""
+@pytest.mark.parametrize("direct_out", ["1", "0"])
+def test_host_pinned_buffers(hb, dev, oracle, monkeypatch, direct_out):
+    """Caller buffers already page-locked: DMA'd directly (no staging copy),
+    the hashes stored by the kernel straight into the output (1) or copied
+    back per chunk (SHF_HB_DIRECT_OUT=0)."""
+    monkeypatch.setenv("SHF_HB_DIRECT_OUT", direct_out)
     lib = hb.load()
     n = 3_000_000
     keys = torch.randint(0, 256, (n * 16,), dtype=torch.uint8).pin_memory()
