@@ -346,6 +346,7 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 struct HostJob {
   shf_hash128* hash = nullptr;
   shf_hash128* hash_dev = nullptr;  // device address of `hash` (page-locked): the kernel stores there
+  bool stage_direct = false;         // else (pageable `hash`): the kernel stores into the slot's pinned staging
   shf_probe* probe = nullptr;
   const shf_row_index* index = nullptr;  // with probe
 };
@@ -367,6 +368,8 @@ int drain_slot(DevCtx* c, int s, Pending& p) {
   return SHF_HB_OK;
 }
 
+void* host_range_device_ptr(const void* p, size_t bytes);
+
 // Kernel output of slot s for `job`, chunk [i0, ...).
 void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k, int* mode) {
   *k = shfhb::Sink();
@@ -378,7 +381,8 @@ void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k,
     k->n_slots = job.index->n_slots;
     *mode = shfhb::kOutProbe;
   } else {
-    k->out = job.hash_dev ? job.hash_dev + i0 : c->d_out[s];
+    void* staged = job.stage_direct ? host_range_device_ptr(c->h_out[s], sizeof(shf_hash128)) : nullptr;
+    k->out = job.hash_dev ? job.hash_dev + i0 : staged ? staged : c->d_out[s];
     *mode = shfhb::kOutHash;
   }
 }
@@ -388,7 +392,10 @@ void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k,
 int job_d2h(DevCtx* c, int s, const HostJob& job, uint64_t i0, uint64_t cnt, bool hash_pinned, bool probe_pinned,
             Pending* p) {
   *p = Pending{true, nullptr, nullptr, cnt};
-  if (job.hash && !job.hash_dev) {
+  if (job.hash && !job.hash_dev && job.stage_direct && !job.probe &&
+      host_range_device_ptr(c->h_out[s], sizeof(shf_hash128))) {
+    p->hash = job.hash + i0;  // the kernel stored into h_out[s] (job_sink): drain_slot copies out
+  } else if (job.hash && !job.hash_dev) {
     HB_TRY(hipMemcpyAsync(hash_pinned ? job.hash + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
                           hipMemcpyDeviceToHost, c->st[s]));
     if (!hash_pinned) p->hash = job.hash + i0;
@@ -467,15 +474,18 @@ void* host_range_device_ptr(const void* p, size_t bytes) {
   return d;
 }
 
-// Staged pipelines with a page-locked hash output: the kernel stores each
-// chunk's hashes straight into it over PCIe (posted writes beside the copy
-// engine's H2D of the next chunk) instead of a D2H copy on the same engine.
-// SHF_HB_DIRECT_OUT=0 turns it off.
+// Staged pipelines: the kernel stores each chunk's hashes over PCIe (posted
+// writes beside the copy engine's H2D of the next chunk) instead of a D2H
+// copy on that same engine -- straight into a page-locked caller output, or
+// into the slot's page-locked staging that drain_slot copies to a pageable
+// one. SHF_HB_DIRECT_OUT=0 turns it off.
 HostJob with_direct_out(const HostJob& job, uint64_t n) {
   HostJob j = job;
   const char* e = getenv("SHF_HB_DIRECT_OUT");
-  if (job.hash && !job.probe && !(e && e[0] == '0'))
+  if (job.hash && !job.probe && !(e && e[0] == '0')) {
     j.hash_dev = static_cast<shf_hash128*>(host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)));
+    j.stage_direct = !j.hash_dev;
+  }
   return j;
 }
 

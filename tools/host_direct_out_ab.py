@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Host-inclusive A/B of SHF_HB_DIRECT_OUT (staged pipelines whose page-locked
-hash output the kernel stores into directly, vs a D2H copy per chunk),
+"""Host-inclusive A/B of SHF_HB_DIRECT_OUT (staged pipelines whose kernel
+stores the hashes into the page-locked output, or the slot's page-locked
+staging for a pageable output, vs a D2H copy per chunk),
 interleaved in one process; outputs of both modes compared.
 
     python tools/host_direct_out_ab.py [--n 10000000] [--reps 5]
@@ -42,7 +43,11 @@ def main():
     poff = torch.from_numpy(off.view(np.int64)).pin_memory()
     outs = {m: {c: torch.empty((nn, 2), dtype=torch.int64).pin_memory() for c, nn in
                 (("fixed16_staged", n), ("fixed256", n256), ("var", n))} for m in "01"}
+    k16p = k16.numpy()
+    outp = {m: np.empty((n, 2), dtype=np.uint64) for m in "01"}
     cases = {
+        "fixed16_pageable": (n, lambda o: lib.shf_hash_batch_fixed(k16p.ctypes.data, 16, n, seed, o.ctypes.data,
+                                                                   hb.MEM_HOST)),
         "fixed16_staged": (n, lambda o: lib.shf_hash_batch_fixed(k16.data_ptr(), 16, n, seed, o.data_ptr(), hb.MEM_HOST)),
         "fixed256": (n256, lambda o: lib.shf_hash_batch_fixed(k256.data_ptr(), 256, n256, seed, o.data_ptr(),
                                                               hb.MEM_HOST)),
@@ -56,13 +61,14 @@ def main():
             for m in "01":
                 os.environ["SHF_HB_DIRECT_OUT"] = m
                 t0 = time.perf_counter()
-                rc = fn(outs[m][c])
+                rc = fn(outp[m] if c == "fixed16_pageable" else outs[m][c])
                 dt = time.perf_counter() - t0
                 assert rc == 0, (c, m, rc)
                 if r:
                     ts[(c, m)].append(dt)
     for c, (nn, _) in cases.items():
-        same = torch.equal(outs["0"][c], outs["1"][c])
+        same = (np.array_equal(outp["0"], outp["1"]) if c == "fixed16_pageable"
+                else torch.equal(outs["0"][c], outs["1"][c]))
         for m in "01":
             t = float(np.median(ts[(c, m)]))
             print("%-16s direct_out=%s  median %8.2f ms  %6.3f G keys/s  outputs equal: %s" % (c, m, t * 1e3,
