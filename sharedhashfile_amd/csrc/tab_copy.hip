@@ -13,17 +13,20 @@
 // names tab_new) or the "keep" image, at the running sum of the record sizes
 // before it in that image; its ref keeps its row and slot.
 //
-// One 512-thread workgroup per tab (a job); thread t owns row t (16 refs,
-// 128 B, read and written with 16-B accesses). Each thread reads its refs and
-// their records' two length words, the workgroup scans the record sizes (keep
-// and move separately: wave shuffles, then the 8 wave totals through LDS),
-// each thread writes its row into both images and copies its records, 8 at a
-// time piece by piece (16-B unaligned loads and stores, so a wave keeps up to
-// 8 of its records' loads in flight per lane; a record's last partial piece is
-// stored exactly), and two waves replay the two images' growth (SHF_TAB_APPEND's
-// tab_size, :562-565) with a wave-wide forward search of the scanned ends.
-// HBM-bound: each record is read once (plus its two length words) and written
-// once, the 64-KiB rows are read once and written twice.
+// One 512-thread workgroup per tab (a job). Record lengths: on packed tabs
+// (no deleted record) the distance from each record's position to the next
+// one's, the 8192 positions bucket-sorted in LDS; otherwise each record's two
+// length words. The refs then go in four segments of 2048 (thread t: refs
+// t + 512 j of each): DPP wave scans of the record sizes per output image,
+// the 8 wave totals through LDS, each ref's row entry written into both
+// images and its record's (end, position) appended to that image's list in
+// LDS, then the data chunks the segment completes are copied (copy_chunks:
+// 16-B destination chunks on consecutive lanes, coalesced full-line stores).
+// The headers' tab_size is a closed form when no record times the growth
+// factor exceeds a page, else two waves replay SHF_TAB_APPEND's growth
+// (:562-565) with a wave-wide forward search of the scanned ends.
+// HBM: each record is read once and written once, the 64-KiB rows are read
+// once (twice on packed tabs, the second from cache) and written twice.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -208,10 +211,12 @@ __device__ __forceinline__ unsigned __int128 put_at(unsigned __int128 out, unsig
 // image's data starts at absolute byte d0 and its records [0, nrec) are in L,
 // `total` bytes of them): consecutive chunks on consecutive lanes of the
 // workgroup, SHFHB_TAB_CHUNKS per lane in flight. A chunk takes its bytes from
-// the record holding its first byte (binary search of the ends) and the next
-// ones where it crosses a record end; a record's first byte is its
-// SHF_DATA_TYPE, written as the job says (shf.c:593-596). Only the data's
-// bytes are written (a chunk straddling its start or end is stored partially).
+// the record holding its first byte and the next ones where it crosses a
+// record end, each loaded 16 B at the address that puts its bytes at their
+// chunk positions, then merged by byte masks (put_at); a record's first byte
+// is its SHF_DATA_TYPE, written as the job says (shf.c:593-596). Only the
+// data's bytes are written (a chunk straddling its start or end is stored
+// partially).
 //
 // A chunk's record: each wave holds 64 consecutive chunks, so one 64-ary
 // search finds the record of its first chunk (r0), every lane loads the end
