@@ -452,6 +452,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         slot[k] = atomicAdd(&counts[(pk[k] - kTabData) / w], 1u);
       }
       seg_barrier();
+      TAB_STAMP(15);
       // exclusive scan of the bucket counts (thread t: buckets [t * kPer, t * kPer + kPer))
       uint32_t c[kPer], sum = 0;
 #pragma unroll

@@ -56,6 +56,9 @@ def main():
     t0 = s[:, 0].min()
     print("workgroups %d, kernel span %.1f us" % (a.n, us(s[:, 14].max() - t0)))
     print("per workgroup: total %.1f us (median)" % us(np.median(s[:, 14] - s[:, 0])))
+    if s[:, 15].any():  # packed tabs: positions loaded and bucket-counted
+        print("seg 0 sort: refs loaded + counted %.1f us, the rest of the sort %.1f us (medians)" %
+              (us(np.median(s[:, 15] - s[:, 0])), us(np.median(s[:, 1] - s[:, 15]))))
     prev = s[:, 0]
     for seg in range(4):
         a1, a2, a3 = s[:, 1 + 3 * seg], s[:, 2 + 3 * seg], s[:, 3 + 3 * seg]
