@@ -144,10 +144,13 @@ SHF_HB_API int shf_hash_batch_var_multi(const void *bytes, const uint64_t *offse
 #define SHF_HB_KERNEL_GENERIC 3 /* any key_len, any alignment, per-lane loads straight from HBM */
 #define SHF_HB_KERNEL_SPAN 4    /* key_len <= 318 (fixed) / any keys (var): LDS-staged spans */
 #define SHF_HB_KERNEL_ROUND 5   /* var only: keys streamed 128 B per round through LDS */
+#define SHF_HB_KERNEL_SPAN_PP 6 /* var only: LDS-staged spans, two tiles per window in turn (what AUTO uses for
+                                   spans over 10 KiB or an unknown byte count); not for probes */
 
 SHF_HB_API int shf_hash_batch_fixed_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                       shf_hash128 *d_out, int kernel, void *hip_stream);
-/* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_ROUND or SHF_HB_KERNEL_GENERIC */
+/* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_SPAN_PP, SHF_HB_KERNEL_ROUND or
+ * SHF_HB_KERNEL_GENERIC */
 SHF_HB_API int shf_hash_batch_var_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                     uint32_t seed, shf_hash128 *d_out, int kernel, void *hip_stream);
 SHF_HB_API int shf_hash_batch_var_sized_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
@@ -299,8 +302,10 @@ SHF_HB_API int shf_tab_part_redirect(uint16_t *map, uint32_t tab_old, uint32_t t
  * Waits for hip_stream (NULL = the null stream), then returns SHF_HB_ERR_ARG if
  * any asynchronous variable-length call (hashing, UID parts or probe) that
  * this thread enqueued on its current device since the previous query met an
- * invalid key (see Conventions), else SHF_HB_OK; the query clears the flag.
- * Calls still running on other streams are reported by a later query. */
+ * invalid key (see Conventions), else SHF_HB_OK; the query clears the flag
+ * (read and cleared in one device-side exchange, so a call still running on
+ * another stream that flags a key after the read is reported by a later query,
+ * never lost). */
 SHF_HB_API int shf_hash_batch_status(void *hip_stream);
 
 /* ---- info ----------------------------------------------------------------- */

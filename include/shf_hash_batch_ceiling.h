@@ -1,0 +1,37 @@
+/*
+ * shf_hash_batch_ceiling.h -- measurement kernels shipped with
+ * libshf_hash_batch.so: the on-box HBM ceilings that bench.py reports each
+ * hashing kernel against (roofline.frac_of_copy_ceiling), and the access
+ * patterns that calibrate rocprofv3's FETCH_SIZE for the probe's row gathers
+ * and the tab copy's unaligned loads. They replace no reference interface:
+ * the reference has no device code. Each kernel moves exactly the bytes of one
+ * hashing kernel's pattern and computes only an XOR fold of what it reads.
+ */
+#ifndef SHF_HASH_BATCH_CEILING_H
+#define SHF_HASH_BATCH_CEILING_H
+
+#include <stdint.h>
+
+#include "shf_hash_batch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* kind: bytes moved per lane (n lanes per launch) */
+#define SHF_HB_CEIL_COPY 0      /* 16-B nt load src[i] + 16-B store dst[i]: k_fixed16's shape, 32 B (src 16-B aligned) */
+#define SHF_HB_CEIL_READ16 1    /* 16 x 16-B nt loads (a wave reads one contiguous 16 KiB) + 16-B store: 272 B;
+                                   n a multiple of 64, src_bytes >= 256 n */
+#define SHF_HB_CEIL_GATHER128 2 /* 4-B idx[i], the 128-B row src[128 idx[i] ..], fetched 8 lanes per row like the
+                                   row pre-probe, + 16-B store: 148 B; every idx[i] < src_bytes / 128 (caller's duty) */
+#define SHF_HB_CEIL_STREAM16U 3 /* 16-B load at src + 16 i + shift (byte-unaligned: shift = 7 for an aligned src)
+                                   + 16-B store: 32 B; src_bytes >= 16 n + 16 */
+
+/* Enqueue one launch on hip_stream. Device pointers; dst 16-B aligned, n x 16 B. */
+SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,
+                                    void *d_dst, uint64_t n, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHF_HASH_BATCH_CEILING_H */

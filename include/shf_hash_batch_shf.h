@@ -83,7 +83,17 @@ static inline int64_t shf_put_batch_var(SHF *shf, const char *bytes, const uint6
  * The index is a snapshot, so a stale candidate only costs the fast path.
  * For every key found, shf_val / shf_val_len hold its value when on_found(ctx, i)
  * is called. Returns the keys found; *fast (if not NULL) = those served by the
- * uid path. */
+ * uid path.
+ *
+ * Concurrency: shf_get_uid_val_copy() copies the value under the window's
+ * reader lock and releases it; the uid path then reads the stored key's length
+ * word (shf_key_addr - 4) and bytes WITHOUT that lock, whereas the reference's
+ * own get compares keys under it (shf.c:933-934). If another thread or process
+ * may delete, re-put or part the same window while this runs, a ref whose
+ * record was replaced in between could pair the old value with a matching new
+ * key. Use the uid path on stores that are quiescent for writers during the
+ * batch (bulk-read phases); otherwise pass probes whose mask is 0 (every key
+ * then takes the locked shf_get_key_val_copy() with the batch hash). */
 static inline uint64_t shf_get_batch_probed(SHF *shf, const char *bytes, const uint64_t *offsets, uint64_t n,
                                             const shf_hash128 *hashes, const shf_probe *probes,
                                             void (*on_found)(void *ctx, uint64_t i), void *ctx, uint64_t *fast)

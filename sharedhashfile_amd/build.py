@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libshf_hash_batch.so")
-SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip"]
+SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip", "hbm_ceiling.hip"]
 HEADERS = ["kernels.h", "murmur3_mix.h"]
 ARCH = "gfx950"
 
@@ -35,7 +35,7 @@ def _stale(target, deps):
 
 def build_library(force=False, verbose=True):
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "shf_hash_batch.h"))
+    deps += [os.path.join(ROOT, "include", h) for h in ("shf_hash_batch.h", "shf_hash_batch_ceiling.h")]
     if not force and not _stale(LIB, deps):
         return LIB
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",

@@ -1,0 +1,121 @@
+// Measurement kernels: the HBM ceilings bench.py divides the hashing kernels'
+// rates by, measured on the same box in the same run (include/shf_hash_batch_ceiling.h).
+// Not part of the hashing path: each kernel moves exactly the bytes of one
+// hashing kernel's access pattern and computes nothing but an XOR fold.
+//
+//   k_ceil_copy      lane i: one 16-B nontemporal load of src[i], one 16-B store
+//                    to dst[i]; 256-thread blocks, one lane per 16 B -- k_fixed16's
+//                    shape (configs[1]) without the hash. 32 B per lane.
+//   k_ceil_read16    lane i: 16 x 16-B nontemporal loads (its wave reads one
+//                    contiguous 16-KiB span, 1 KiB per instruction, the way k_tiled
+//                    and k_span stage a tile), their XOR stored as 16 B. 272 B per
+//                    lane: configs[2]'s 256 + 16 B per key (configs[3]: 284).
+//   k_ceil_gather128 lane i: one 128-B row rows[idx[i]] (the row index read as a
+//                    4-B stream), fetched 8 lanes per row exactly as the probe's
+//                    row fetch does (probe_scan_coop), 16 B stored per lane. With
+//                    idx a permutation every row is read once: 148 B per lane.
+//   k_ceil_stream16u lane i: one 16-B load at src + 16 i + shift (shift 1..15:
+//                    byte-unaligned, as the tab copy's record gathers load), one
+//                    16-B store to dst[i]. 32 B per lane, each source line read
+//                    once (a calibration of FETCH_SIZE for unaligned loads).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/shf_hash_batch_ceiling.h"
+
+namespace shfhb {
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) const u32x4_a1 g_u32x4_a1;
+
+constexpr uint32_t kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void k_ceil_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                      uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  dst[i] = __builtin_nontemporal_load(&src[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ceil_read16(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                        uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t wave = i >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (wave * 64u >= n) return;  // whole waves only: n is a multiple of 64 (checked by the launcher)
+  const u32x4* span = src + wave * 64u * 16u;
+  u32x4 v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = __builtin_nontemporal_load(&span[64 * q + lane]);
+  u32x4 x = v[0];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) x ^= v[q];
+  dst[i] = x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __restrict__ rows,
+                                                           const uint32_t* __restrict__ idx, u32x4* __restrict__ dst,
+                                                           uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t r = i < n ? __builtin_nontemporal_load(&idx[i]) : 0u;  // lanes past n fetch row 0 and discard it
+  u32x4 g[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t rq = (uint32_t)__shfl((int)r, (int)(8u * q + (lane >> 3)));
+    g[q] = *reinterpret_cast<g_u32x4*>(reinterpret_cast<uintptr_t>(rows) + ((uint64_t)rq << 7) + 16u * (lane & 7u));
+  }
+  u32x4 x = g[0];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) x ^= g[q];
+  if (i < n) dst[i] = x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ceil_stream16u(const uint8_t* __restrict__ src, u32x4* __restrict__ dst,
+                                                           uint64_t n, uint32_t shift) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  dst[i] = *reinterpret_cast<g_u32x4_a1*>(reinterpret_cast<uintptr_t>(src) + 16u * i + shift);
+}
+
+}  // namespace
+}  // namespace shfhb
+
+extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_bytes, const uint32_t* d_idx,
+                                    void* d_dst, uint64_t n, void* hip_stream) {
+  using namespace shfhb;
+  if (n == 0) return SHF_HB_OK;
+  if (!d_src || !d_dst || (n + kBlock - 1) / kBlock > 0x7fffffffull) return SHF_HB_ERR_ARG;
+  if (((uintptr_t)d_dst & 15u) != 0) return SHF_HB_ERR_ARG;
+  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
+  const hipStream_t st = (hipStream_t)hip_stream;
+  const bool al16 = ((uintptr_t)d_src & 15u) == 0;
+  switch (kind) {
+    case SHF_HB_CEIL_COPY:
+      if (!al16 || src_bytes < 16u * n) return SHF_HB_ERR_ARG;
+      hipLaunchKernelGGL(k_ceil_copy, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
+      break;
+    case SHF_HB_CEIL_READ16:
+      if (!al16 || n % 64u || src_bytes < 256u * n) return SHF_HB_ERR_ARG;
+      hipLaunchKernelGGL(k_ceil_read16, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
+      break;
+    case SHF_HB_CEIL_GATHER128:
+      // every idx[i] must name a row inside src: checked by the caller's construction (a permutation
+      // of src_bytes / 128 rows), not here -- the launcher cannot read device memory
+      if (!al16 || !d_idx || src_bytes < 128u || src_bytes / 128u > 0xffffffffull) return SHF_HB_ERR_ARG;
+      hipLaunchKernelGGL(k_ceil_gather128, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
+      break;
+    case SHF_HB_CEIL_STREAM16U: {
+      const uint32_t shift = (uint32_t)(((uintptr_t)d_src) & 15u) ? 0u : 7u;  // aligned base: read 7 bytes in
+      if (src_bytes < 16u * n + 16u) return SHF_HB_ERR_ARG;
+      hipLaunchKernelGGL(k_ceil_stream16u, grid, block, 0, st, (const uint8_t*)d_src, (u32x4*)d_dst, n, shift);
+      break;
+    }
+    default:
+      return SHF_HB_ERR_ARG;
+  }
+  return hipGetLastError() == hipSuccess ? SHF_HB_OK : SHF_HB_ERR_HIP;
+}

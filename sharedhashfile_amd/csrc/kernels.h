@@ -18,7 +18,8 @@ enum KernelChoice {
   kKernelTiled = 2,
   kKernelGeneric = 3,
   kKernelSpan = 4,
-  kKernelRound = 5
+  kKernelRound = 5,
+  kKernelSpanPP = 6
 };
 
 // Where a kernel's per-key result goes (passed by value as a kernel argument).
@@ -41,6 +42,9 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
                       const Sink& sink, int out_mode, hipStream_t st, int kernel = kKernelAuto,
                       uint64_t key_bytes = 0);
+
+// *taken = atomic exchange of *word with 0 (one thread).
+hipError_t launch_status_take(uint32_t* word, uint32_t* taken, hipStream_t st);
 
 // Row pre-probe of precomputed hashes (n x 16 B on device) into sink.out.
 hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st);

@@ -31,7 +31,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <atomic>
 
 #include "murmur3_mix.h"
 #include "kernels.h"
@@ -127,15 +126,12 @@ __device__ __forceinline__ u32x4 probe_scan(const Sink& k, const ProbeLoc& p) {
 
 __device__ __forceinline__ u32x4 probe_row(const Sink& k, const State& s) { return probe_scan(k, probe_locate(k, s)); }
 
-#ifndef SHFHB_PROBE_LDS
-#define SHFHB_PROBE_LDS 1  // cooperative row fetch + LDS transpose: +3 % (profiles/r1/ab_probe_lds/)
-#endif
-
 // probe_scan for a whole wave (every lane must call it): the rows are fetched
 // 8 lanes per row, so each of the 8 load instructions touches 8 whole 128-B
 // lines instead of 64 partial ones (row addresses move by __shfl), then
 // transposed through `lds` (8 KiB for this wave, XOR-swizzled so both the
-// ds_write_b128 and the ds_read_b128 are conflict-free) for the lane's compares.
+// ds_write_b128 and the ds_read_b128 are conflict-free) for the lane's compares:
+// +3 % over per-lane row loads (profiles/r1/ab_probe_lds/).
 __device__ __forceinline__ u32x4 probe_scan_coop(const Sink& k, const ProbeLoc& p, u32x4* lds) {
   const uint32_t lane = __lane_id();
   const uint64_t at = probe_row_addr(k, p);
@@ -186,19 +182,12 @@ __device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const
 // ballots and ds_bpermute -- measured 3.9x slower: profiles/r1/ab_probe_coop_vs_lane_*.txt.)
 __global__ __launch_bounds__(256) void k_probe_hashes(const u32x4* __restrict__ hashes, uint64_t n, Sink sink) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#if SHFHB_PROBE_LDS
   __shared__ u32x4 rows_lds[256 * 8];
   u32x4 h = {0u, 0u, 0u, 0u};  // lanes past n still take part in the wave's row fetch
   if (i < n) h = __builtin_nontemporal_load(&hashes[i]);
   const State s{pack64(h.x, h.y), pack64(h.z, h.w)};
   const u32x4 rec = probe_scan_coop(sink, probe_locate(sink, s), rows_lds + (threadIdx.x & ~63u) * 8u);
   if (i < n) reinterpret_cast<u32x4*>(sink.out)[i] = rec;
-#else
-  if (i >= n) return;
-  const u32x4 h = __builtin_nontemporal_load(&hashes[i]);
-  const State s{pack64(h.x, h.y), pack64(h.z, h.w)};
-  reinterpret_cast<u32x4*>(sink.out)[i] = probe_row(sink, s);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -219,79 +208,33 @@ __device__ __forceinline__ void flag_bad_key(const Sink& sink) {
 // One key per lane and as many workgroups as keys need: no grid-stride loop
 // (6.36 vs 5.16 TB/s at 100M keys against a 8192-block grid-stride loop,
 // profiles/r1/ab_fixed16.txt; a loop that runs once measured the same,
-// profiles/r1/ab_fixed16_noloop_*.txt). OUT = kOutProbe is the fused
-// hash + row pre-probe.
-#ifndef SHFHB_F16_BLOCK
-#define SHFHB_F16_BLOCK 256
-#endif
-#ifndef SHFHB_F16_KPL
-#define SHFHB_F16_KPL 1  // keys per lane (strided by the block size)
-#endif
-#ifndef SHFHB_F16_NTSTORE
-#define SHFHB_F16_NTSTORE 0
-#endif
-constexpr uint32_t kF16Block = SHFHB_F16_BLOCK;
-constexpr uint32_t kF16Kpl = SHFHB_F16_KPL;
-#ifndef SHFHB_PROBE_KPL
-#define SHFHB_PROBE_KPL 1  // keys per lane of the fused hash + row pre-probe (2 and 4 measured ~2 % slower)
-#endif
-template <int OUT>
-constexpr uint32_t kF16KplOf = OUT == kOutProbe ? (uint32_t)SHFHB_PROBE_KPL : kF16Kpl;
+// profiles/r1/ab_fixed16_noloop_*.txt). 128/512/1024 threads per block, two keys
+// per lane and nontemporal stores all measured within 3 % of this shape
+// (profiles/r1/ab_fixed16_shapes/); two or four keys per lane in the fused
+// probe ~2 % slower. OUT = kOutProbe is the fused hash + row pre-probe.
+constexpr uint32_t kF16Block = 256;
 
 template <int OUT>
 __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
                                                        Sink sink) {
-  constexpr uint32_t kpl = kF16KplOf<OUT>;
-  const uint64_t i0 = (uint64_t)blockIdx.x * (kF16Block * kpl) + threadIdx.x;
-  u32x4 k[kpl];
-#pragma unroll
-  for (uint32_t j = 0; j < kpl; ++j) {
-    const uint64_t i = i0 + j * kF16Block;
-    k[j] = u32x4{0u, 0u, 0u, 0u};
-    if (i < n) k[j] = __builtin_nontemporal_load(&keys[i]);
-  }
+  const uint64_t i = (uint64_t)blockIdx.x * kF16Block + threadIdx.x;
   if constexpr (OUT == kOutProbe) {
-    // every key's tab-map lookup, then every key's row scan, then the stores: no
-    // store sits between two keys' loads, so all their rows are in flight together
-    State s[kpl];
-    ProbeLoc p[kpl];
-    u32x4 rec[kpl];
-#pragma unroll
-    for (uint32_t j = 0; j < kpl; ++j) {
-      s[j] = State{seed, seed};
-      body_block(s[j], pack64(k[j].x, k[j].y), pack64(k[j].z, k[j].w));
-      finish(s[j], 16);
-      p[j] = probe_locate(sink, s[j]);
-    }
-#if SHFHB_PROBE_LDS
-    static_assert(kpl == 1, "one key per lane");
+    // every lane of the wave takes part in the cooperative row fetch
+    const u32x4 k = i < n ? __builtin_nontemporal_load(&keys[i]) : u32x4{0u, 0u, 0u, 0u};
+    State s{seed, seed};
+    body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
+    finish(s, 16);
     __shared__ u32x4 rows_lds[kF16Block * 8];
-    rec[0] = probe_scan_coop(sink, p[0], rows_lds + (threadIdx.x & ~63u) * 8u);
-#else
-#pragma unroll
-    for (uint32_t j = 0; j < kpl; ++j) rec[j] = probe_scan(sink, p[j]);
-#endif
-#pragma unroll
-    for (uint32_t j = 0; j < kpl; ++j) {
-      const uint64_t i = i0 + j * kF16Block;
-      if (i < n) store_probe(sink, i, s[j], rec[j]);
-    }
+    const u32x4 rec = probe_scan_coop(sink, probe_locate(sink, s), rows_lds + (threadIdx.x & ~63u) * 8u);
+    if (i < n) store_probe(sink, i, s, rec);
     return;
   }
-#pragma unroll
-  for (uint32_t j = 0; j < kpl; ++j) {
-    const uint64_t i = i0 + j * kF16Block;
-    if (i >= n) return;
-    State s{seed, seed};
-    body_block(s, pack64(k[j].x, k[j].y), pack64(k[j].z, k[j].w));
-    finish(s, 16);
-    if constexpr (OUT == kOutHash && SHFHB_F16_NTSTORE) {
-      const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + i);
-    } else {
-      store_result<OUT>(sink, i, s);
-    }
-  }
+  if (i >= n) return;
+  const u32x4 k = __builtin_nontemporal_load(&keys[i]);
+  State s{seed, seed};
+  body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
+  finish(s, 16);
+  store_result<OUT>(sink, i, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -354,9 +297,7 @@ __device__ __forceinline__ State hash_bytes(const uint8_t* p, uint32_t len, uint
   return s;
 }
 
-#ifndef SHFHB_GENERIC_GRID_CAP
-#define SHFHB_GENERIC_GRID_CAP (1u << 20)  // one key per lane: 5.57 vs 5.19 TB/s at 32-B keys
-#endif
+constexpr unsigned kGenericGridCap = 1u << 20;  // one key per lane: 5.57 vs 5.19 TB/s at 32-B keys
 template <int OUT, bool VAR>
 __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ bytes,
                                                  const uint64_t* __restrict__ offsets, uint64_t off_base,
@@ -398,17 +339,11 @@ __global__ __launch_bounds__(256) void k_generic(const uint8_t* __restrict__ byt
 // while hashing round r out of LDS.
 // ---------------------------------------------------------------------------
 constexpr int kTileKeys = 64;
-#ifndef SHFHB_TILED_WAVES
-#define SHFHB_TILED_WAVES 1  // one wave per workgroup measured 4 % faster than 4 at 100M x 256 B
-#endif
-constexpr int kTiledWaves = SHFHB_TILED_WAVES;  // waves per workgroup
-#ifndef SHFHB_TILED_GRID_MULT
-#define SHFHB_TILED_GRID_MULT 0  // grid = this many x the resident workgroups (0: one tile per wave;
-                                 // 6.09 vs 5.05 TB/s at 100M x 256 B, profiles/r1/ab_tiled_grid.txt)
-#endif
-#ifndef SHFHB_TILED_BATCH
-#define SHFHB_TILED_BATCH 8  // LDS blocks read per batch in k_tiled
-#endif
+// One wave per workgroup (4 % faster than 4 at 100M x 256 B) and one tile per
+// wave: a grid of as many workgroups as tiles (6.09 vs 5.05 TB/s for a
+// persistent grid of the resident workgroups, profiles/r1/ab_tiled_grid.txt).
+constexpr int kTiledWaves = 1;  // waves per workgroup
+constexpr int kTiledBatchMax = 8;  // LDS blocks read at once (all 8 beat smaller batches: 5.43 vs 4.94 TB/s)
 
 // LDS slot of piece j of key k for R pieces (16 B each) per key per round. The
 // XOR term spreads the 16 lanes of each ds_read_b128 lane group (which always
@@ -423,7 +358,7 @@ template <int OUT, int R>
 __global__ __launch_bounds__(64 * kTiledWaves) void k_tiled(const uint8_t* __restrict__ keys, uint32_t key_len,
                                                             uint64_t n, uint32_t seed, Sink sink) {
   static_assert(R == 4 || R == 8 || R == 16, "pieces per key per round");
-  constexpr int kTiledBatch = SHFHB_TILED_BATCH < R ? SHFHB_TILED_BATCH : R;
+  constexpr int kTiledBatch = kTiledBatchMax < R ? kTiledBatchMax : R;
   constexpr uint32_t kKeysPerInstr = 64 / R;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kTiledWaves][kTileKeys * R * 16];
   const uint32_t lane = threadIdx.x & 63u;
@@ -704,17 +639,12 @@ __device__ __forceinline__ State hash_lds(const uint32_t* lds, uint32_t p, uint3
   return s;
 }
 
-#ifndef SHFHB_LDS_UNALIGNED
-#define SHFHB_LDS_UNALIGNED 1  // variable-length k_span: U[8,512] B keys +4-8 % (profiles/r2/ab_span/)
-#endif
-#ifndef SHFHB_SPAN_PINGPONG
-#define SHFHB_SPAN_PINGPONG 1  // k_span_pp for variable-length windows over 10 KiB
-#endif
 
 
 // hash_lds with one unaligned ds_read_b128 per block instead of dword reads
 // funnel-shifted by v_alignbyte_b32 (gfx950 runs LDS accesses in unaligned
-// mode; hipcc emits ds_read_b128 for an align-1 vector LDS load).
+// mode; hipcc emits ds_read_b128 for an align-1 vector LDS load). Variable
+// lengths: U[8,512] B keys +4-8 % (profiles/r2/ab_span/).
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 typedef __attribute__((address_space(3))) const u32x4_a1 lds_u32x4_a1;
@@ -769,9 +699,6 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
 constexpr int kVrPieces = 9;                     // 16-B pieces per key per round
 constexpr uint32_t kVrWindow = kVrPieces * 16u;  // 144 B
 constexpr uint32_t kVrMaxRounds = 64;            // keys up to 8 KiB in the staged path
-#ifndef SHFHB_VR_NT
-#define SHFHB_VR_NT 0
-#endif
 
 // Hash the blocks of round r of a key from its LDS window: window bytes
 // [sh16, sh16 + 128) are key bytes [128r, 128r + 128). All 36 dwords the
@@ -861,12 +788,10 @@ __device__ __forceinline__ void vround_tile(const uint8_t* bytes, uint64_t key, 
 #pragma unroll
     for (int q = 0; q < kVrPieces; ++q) {
       reg[q] = u32x4{0u, 0u, 0u, 0u};
-      if (128u * r < lend[q])  // the piece starts inside the key: its aligned 16 B cannot leave the key's page
-#if SHFHB_VR_NT
-        reg[q] = __builtin_nontemporal_load(reinterpret_cast<g_u32x4*>(tile0 + lrel[q] + 128u * r));
-#else  // keep lines in L2: the window's last piece is the next round's first
-        reg[q] = *reinterpret_cast<g_u32x4*>(tile0 + lrel[q] + 128u * r);
-#endif
+      // the piece starts inside the key: its aligned 16 B cannot leave the key's page. Plain
+      // (not nt) loads keep lines in L2: the window's last piece is the next round's first
+      // (nt: 2.56 vs 1.59 ms at 25M x 260 B, profiles/r1/ab_vround_nt.txt)
+      if (128u * r < lend[q]) reg[q] = *reinterpret_cast<g_u32x4*>(tile0 + lrel[q] + 128u * r);
     }
   };
   u32x4 nxt[kVrPieces];
@@ -940,7 +865,7 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
       const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base);
       // variable lengths: unaligned 16-B reads; fixed lengths keep the dword reads (L = 100, 200, 300 B:
       // 4, 2, 9 % faster that way, profiles/r2/ab_span/)
-      store_result<OUT>(sink, ti.key, (SHFHB_LDS_UNALIGNED && VAR) ? hash_lds_u(span_lds, p, ti.len, seed)
+      store_result<OUT>(sink, ti.key, VAR ? hash_lds_u(span_lds, p, ti.len, seed)
                                                                    : hash_lds(span_lds, p, ti.len, seed));
     }
   } else if constexpr (VAR && RFB) {  // span over the window: stream it in rounds (vround_tile) instead
@@ -959,9 +884,9 @@ __global__ __launch_bounds__(64, 4) void k_span(const uint8_t* __restrict__ byte
 // staged or hashed (one HBM latency per two tiles instead of one per tile),
 // and a CU keeps twice as many hashing waves (4 per SIMD) for the same LDS.
 // U[8,512] B keys: +10 %, all-260 B: +15 %, U[200,400] B: +12 % over k_span
-// (profiles/r2/ab_span/). Tiles with an invalid key or a span over the window
-// are hashed per lane straight from HBM (few registers: the held span and the
-// hash must fit 128 VGPRs together).
+// (profiles/r2/ab_span/). A tile whose span is over the window is streamed
+// through it in rounds (vround_tile) in its wave's turn; a tile with an invalid
+// key is hashed per lane straight from HBM.
 // (Two or more tiles per wave, each wave loading its next span right after
 // its hash, spill past 128 VGPRs; a persistent single-wave variant with the
 // next span prefetched into registers during the hash measured 0-10 % slower
@@ -1012,46 +937,40 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool bad = __ballot(var_key_bad(raw.o0, raw.o1)) != 0;
   const SpanTile<true> ti = span_finish<true>(bytes, off_base, 0, n, raw, lane);
   const bool staged = has && !bad && ti.span16 <= cap;
-  u32x4 reg[PIECES];
-  if (staged) span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
   // Wave 0 stages and hashes; one barrier hands the window to wave 1, which
   // stages and hashes in turn (a wave's own LDS writes and reads are ordered
   // by a wave-level fence). One barrier instead of the four of two
   // stage/hash phases: U[8,512] +1.7 %, all-260 B +10.6 %, U[200,400] +4.7 %
-  // (profiles/r2/ab_span/ab_handoff2, "t32").
-  if (wave == 0 && staged) {
-    span_stage<PIECES>(span_lds, reg, ti.span16, lane);
-    wave_lds_fence();
-    span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
+  // (profiles/r2/ab_span/ab_handoff2, "t32"). Each wave passes exactly one
+  // barrier on either branch; the held span lives only on the staged one, so
+  // the round fallback's registers never sit beside it.
+  if (staged) {
+    u32x4 reg[PIECES];
+    span_fetch<PIECES>(reg, ti.base, ti.span16, lane);
+    if (wave == 0) {
+      span_stage<PIECES>(span_lds, reg, ti.span16, lane);
+      wave_lds_fence();
+      span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
+    }
+    lds_barrier();  // wave 0 is done with the window (its result stores may still be in flight)
+    if (wave == 1) {
+      span_stage<PIECES>(span_lds, reg, ti.span16, lane);
+      wave_lds_fence();
+      span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
+    }
+  } else {
+    const bool over = has && !bad;  // span over the window: streamed through it in rounds, in this wave's turn
+    uint8_t* win = reinterpret_cast<uint8_t*>(span_lds);
+    if (wave == 0 && over) vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, win);
+    lds_barrier();
+    if (wave == 1 && over) vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, win);
+    if (has && bad) span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
   }
-  lds_barrier();  // wave 0 is done with the window (its result stores may still be in flight)
-  if (wave == 1 && staged) {
-    span_stage<PIECES>(span_lds, reg, ti.span16, lane);
-    wave_lds_fence();
-    span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
-  }
-  if (has && !staged) span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
 }
 
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-// Workgroups of `kernel` that fit on the whole device at once (cached per device).
-static unsigned resident_grid(const void* kernel, int block, size_t dyn_lds, int slot) {
-  static std::atomic<unsigned> cache[16][32];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-  unsigned g = cache[dev][slot].load(std::memory_order_relaxed);
-  if (g) return g;
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-  g = (unsigned)(per_cu * cus);
-  cache[dev][slot].store(g, std::memory_order_relaxed);
-  return g;
-}
-
 // Pieces (16 B) of every key staged per round by k_tiled. 8 (one 128-B line per
 // key per round) when every round is full; otherwise 16, so that a key of
 // 12-15 pieces is one round instead of a full and a mostly empty one
@@ -1100,6 +1019,7 @@ constexpr uint32_t kLdsPerCu = 160u * 1024u;
 template <int OUT>
 static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
                                            uint32_t seed, const Sink& sink, hipStream_t st) {
+  static_assert(kSpanAlloc - kSpanPad >= kVrLdsBytes, "the window holds the round fallback's LDS");
   const uint64_t tiles = (n + 63) / 64;
   const uint64_t wgs = (tiles + 1) / 2;
   if (wgs > 0x7fffffffull) return hipErrorInvalidValue;
@@ -1128,14 +1048,17 @@ static hipError_t launch_var_span(const void* bytes, const uint64_t* offsets, ui
 
 // Fixed lengths: a tile's span is at most 64 * key_len + 15 bytes, so the LDS
 // request (and the fetch) is sized to that; variable lengths use the window.
+// pingpong: AUTO may take k_span_pp (a forced SHF_HB_KERNEL_SPAN keeps k_span).
 template <int OUT, bool VAR>
 static hipError_t launch_span(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint32_t key_len,
-                              uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0) {
+                              uint64_t n, uint32_t seed, const Sink& sink, hipStream_t st, uint64_t key_bytes = 0,
+                              bool pingpong = false) {
   if constexpr (VAR) {
     const double need = key_bytes && n ? 64.0 * (double)key_bytes / (double)n * 1.1 + 512.0 + kSpanPad : 1e30;
-    // windows over 10 KiB (config D's U[8,512] B keys): two waves per window
+    // windows over 10 KiB (config D's U[8,512] B keys) or an unknown byte count: two waves per
+    // window, overflowing tiles streamed in rounds through it
     if constexpr (OUT != kOutProbe)
-      if (SHFHB_SPAN_PINGPONG && need > 10240.0 + kSpanPad)
+      if (pingpong && need > 10240.0 + kSpanPad)
         return launch_var_span_pingpong<OUT>(bytes, offsets, off_base, n, seed, sink, st);
     if (need >= (double)kSpanAlloc)
       return launch_span_p<OUT, VAR, kSpanPiecesMax>(bytes, offsets, off_base, 0, n, seed, sink, st, kSpanAlloc);
@@ -1180,7 +1103,7 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   switch (kernel) {
     case kKernelFixed16:
     {
-      constexpr uint64_t per_block = (uint64_t)kF16Block * kF16KplOf<OUT>;
+      constexpr uint64_t per_block = kF16Block;
       if (key_len != 16 || !al16 || (n + per_block - 1) / per_block > 0x7fffffffull) return hipErrorInvalidValue;
       hipLaunchKernelGGL(k_fixed16<OUT>, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(kF16Block), 0, st,
                          reinterpret_cast<const u32x4*>(keys), n, seed, sink);
@@ -1190,12 +1113,7 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
       if (key_len < 32 || (key_len & 15u) || !al16) return hipErrorInvalidValue;
       const uint64_t tiles = (n + kTileKeys - 1) / kTileKeys;
       const int r = tiled_round_pieces(key_len);
-      const void* fn = r == 4    ? reinterpret_cast<const void*>(&k_tiled<OUT, 4>)
-                       : r == 16 ? reinterpret_cast<const void*>(&k_tiled<OUT, 16>)
-                                 : reinterpret_cast<const void*>(&k_tiled<OUT, 8>);
-      const unsigned res = resident_grid(fn, 64 * kTiledWaves, 0, 6 + OUT * 3 + (r == 4 ? 0 : r == 8 ? 1 : 2));
-      const dim3 g(grid_for(tiles, kTiledWaves, SHFHB_TILED_GRID_MULT ? res * SHFHB_TILED_GRID_MULT : 0xffffffffu)),
-          b(64 * kTiledWaves);
+      const dim3 g(grid_for(tiles, kTiledWaves, 0xffffffffu)), b(64 * kTiledWaves);
       const uint8_t* k8 = reinterpret_cast<const uint8_t*>(keys);
       if (r == 4) hipLaunchKernelGGL((k_tiled<OUT, 4>), g, b, 0, st, k8, key_len, n, seed, sink);
       else if (r == 16) hipLaunchKernelGGL((k_tiled<OUT, 16>), g, b, 0, st, k8, key_len, n, seed, sink);
@@ -1205,7 +1123,7 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
     case kKernelSpan:
       return launch_span<OUT, false>(keys, nullptr, 0, key_len, n, seed, sink, st);
     default:
-      hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
+      hipLaunchKernelGGL((k_generic<OUT, false>), dim3(grid_for(n, 256, kGenericGridCap)), dim3(256), 0, st,
                          reinterpret_cast<const uint8_t*>(keys), (const uint64_t*)nullptr, (uint64_t)0, key_len, n,
                          seed, sink);
       break;
@@ -1222,7 +1140,7 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
   // span 3247 GB/s).
   if (kernel == kKernelAuto && key_bytes != 0 && key_bytes / n > 300) kernel = kKernelRound;
   if (kernel == kKernelGeneric) {
-    hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, SHFHB_GENERIC_GRID_CAP)), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_generic<OUT, true>), dim3(grid_for(n, 256, kGenericGridCap)), dim3(256), 0, st,
                        reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, (uint32_t)0, n, seed, sink);
     return hipGetLastError();
   }
@@ -1233,7 +1151,11 @@ static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint6
                        offsets, off_base, n, seed, sink);
     return hipGetLastError();
   }
-  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st, key_bytes);
+  if (kernel == kKernelSpanPP) {
+    if constexpr (OUT == kOutProbe) return hipErrorInvalidValue;
+    else return launch_var_span_pingpong<OUT>(bytes, offsets, off_base, n, seed, sink, st);
+  }
+  return launch_span<OUT, true>(bytes, offsets, off_base, 0, n, seed, sink, st, key_bytes, kernel == kKernelAuto);
 }
 
 hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
@@ -1260,6 +1182,15 @@ hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_b
     default:
       return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
   }
+}
+
+__global__ __launch_bounds__(64) void k_status_take(uint32_t* word, uint32_t* taken) {
+  if (threadIdx.x == 0) *taken = atomicExch(word, 0u);
+}
+
+hipError_t launch_status_take(uint32_t* word, uint32_t* taken, hipStream_t st) {
+  hipLaunchKernelGGL(k_status_take, dim3(1), dim3(64), 0, st, word, taken);
+  return hipGetLastError();
 }
 
 hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st) {

@@ -33,30 +33,22 @@ __device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
 // Rotates as two v_alignbit_b32 and `x * 5` as one v_lshl_add_u64, with the
 // h1/h2 chain left undistributed (two *5 per block instead of four): k_span
 // +7.8 %, k_vround +5.2 % on U[8,512] keys, fixed-length kernels unchanged
-// (HBM-bound) -- profiles/r1/ab_asm/. 0 keeps the compiler's own lowering.
-#ifndef SHFHB_ASM_MIX
-#define SHFHB_ASM_MIX 1
-#endif
-#if SHFHB_ASM_MIX
-// r is a compile-time constant after inlining: two v_alignbit_b32 (the
-// compiler's own lowering is a 64-bit shift, a 32-bit shift and an or).
+// (HBM-bound) -- profiles/r1/ab_asm/. (The compiler's own lowering -- a 64-bit
+// shift, a 32-bit shift and an or per rotate, two v_mad_u64_u32 per *5 -- is in
+// git history.)
+// r is a compile-time constant after inlining.
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   if (r < 32)
     return pack64(__builtin_amdgcn_alignbit(lo, hi, 32 - r), __builtin_amdgcn_alignbit(hi, lo, 32 - r));
   return pack64(__builtin_amdgcn_alignbit(hi, lo, 64 - r), __builtin_amdgcn_alignbit(lo, hi, 64 - r));
 }
-// x * 5 as one v_lshl_add_u64 (x << 2) + x; the compiler's lowering of a
-// multiply by 5 is two v_mad_u64_u32.
+// x * 5 as one v_lshl_add_u64 (x << 2) + x.
 __device__ __forceinline__ uint64_t mul5(uint64_t x) {
   uint64_t r;
   asm("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(r) : "v"(x));
   return r;
 }
-#else
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-__device__ __forceinline__ uint64_t mul5(uint64_t x) { return x * 5; }
-#endif
 
 __device__ __forceinline__ uint64_t mix_k1(uint64_t k) { return rotl64(k * kC1, 31) * kC2; }
 __device__ __forceinline__ uint64_t mix_k2(uint64_t k) { return rotl64(k * kC2, 33) * kC1; }
@@ -68,30 +60,9 @@ struct State {
 // One 16-byte body block whose k1/k2 are already mixed (murmurhash3.c:97-103):
 //   h1 = (rotl(h1 ^ m1, 27) + h2) * 5 + N1
 //   h2 = (rotl(h2 ^ m2, 31) + h1) * 5 + N2
-// distributed (mod 2^64) as
-//   h1' = rotl(h1 ^ m1, 27) * 5 + (h2 * 5 + N1)
-//   h2' = rotl(h2 ^ m2, 31) * 5 + (h1' * 5 + N2)
-// so everything but `h1' * 5 + N2 + ...` is off the serial h1 -> h2 -> h1 path:
-// the chain across blocks is the latency bound of a lane, not its op count.
-#ifndef SHFHB_CHAIN_DISTRIBUTED
-#define SHFHB_CHAIN_DISTRIBUTED 1
-#endif
 __device__ __forceinline__ void chain_block(State& s, uint64_t m1, uint64_t m2) {
-#if SHFHB_ASM_MIX
   s.h1 = mul5(rotl64(s.h1 ^ m1, 27) + s.h2) + kN1;
   s.h2 = mul5(rotl64(s.h2 ^ m2, 31) + s.h1) + kN2;
-#elif SHFHB_CHAIN_DISTRIBUTED
-  const uint64_t a1 = rotl64(s.h1 ^ m1, 27) * 5;
-  const uint64_t b1 = s.h2 * 5 + kN1;
-  const uint64_t a2 = rotl64(s.h2 ^ m2, 31) * 5;
-  s.h1 = a1 + b1;
-  s.h2 = a2 + (s.h1 * 5 + kN2);
-#else
-  s.h1 ^= m1;
-  s.h1 = (rotl64(s.h1, 27) + s.h2) * 5 + kN1;
-  s.h2 ^= m2;
-  s.h2 = (rotl64(s.h2, 31) + s.h1) * 5 + kN2;
-#endif
 }
 
 __device__ __forceinline__ void body_block(State& s, uint64_t k1, uint64_t k2) {

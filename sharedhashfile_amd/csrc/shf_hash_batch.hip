@@ -107,7 +107,8 @@ struct DevCtx {
   int n_staged = 0;  // slots whose staging buffers are allocated
   // Variable-length key checks done by the kernels (kernels.h Sink::status):
   // word 0 collects this thread's async calls until shf_hash_batch_status()
-  // reads it, word 1 is cleared and read by each synchronous call.
+  // takes it (word 2 receives the taken value), word 1 is cleared and read by
+  // each synchronous call.
   uint32_t* d_status = nullptr;
   uint32_t* h_status = nullptr;  // pinned, 1 word
 };
@@ -155,8 +156,8 @@ int current_ctx(DevCtx** out) {
       c->status = map_hip(hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking));
       if (c->status == SHF_HB_OK) c->status = map_hip(hipEventCreateWithFlags(&c->done[s], hipEventDisableTiming));
     }
-    if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 2 * sizeof(uint32_t)));
-    if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 2 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 3 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
     if (c->status == SHF_HB_OK)
       c->status = map_hip(hipHostMalloc((void**)&c->h_status, sizeof(uint32_t), hipHostMallocDefault));
   }
@@ -680,6 +681,11 @@ int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t 
   return SHF_HB_OK;
 }
 
+bool var_kernel_valid(int kernel) {
+  return kernel == SHF_HB_KERNEL_AUTO || kernel == SHF_HB_KERNEL_SPAN || kernel == SHF_HB_KERNEL_SPAN_PP ||
+         kernel == SHF_HB_KERNEL_GENERIC || kernel == SHF_HB_KERNEL_ROUND;
+}
+
 // Can the forced fixed-length kernel take this shape? (AUTO always can.)
 bool fixed_kernel_fits(const void* d_keys, uint32_t key_len, int kernel) {
   const bool al16 = ((uintptr_t)d_keys & 15u) == 0;
@@ -818,9 +824,7 @@ int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offse
                                     shf_hash128* d_out, int kernel, void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
-  if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC &&
-      kernel != SHF_HB_KERNEL_ROUND)
-    return SHF_HB_ERR_ARG;
+  if (!var_kernel_valid(kernel)) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false, kernel);
 }
 
@@ -837,9 +841,7 @@ int shf_hash_batch_var_sized_kernel_async(const void* d_bytes, const uint64_t* d
                                           void* hip_stream) {
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
-  if (kernel != SHF_HB_KERNEL_AUTO && kernel != SHF_HB_KERNEL_SPAN && kernel != SHF_HB_KERNEL_GENERIC &&
-      kernel != SHF_HB_KERNEL_ROUND)
-    return SHF_HB_ERR_ARG;
+  if (!var_kernel_valid(kernel)) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false,
                     kernel, key_bytes);
 }
@@ -1081,11 +1083,12 @@ int shf_hash_batch_status(void* hip_stream) {
   int rc = current_ctx(&c);
   if (rc) return rc;
   HB_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
-  uint32_t v = 0;
-  HB_TRY(hipMemcpy(&v, c->d_status, sizeof(v), hipMemcpyDeviceToHost));
-  if (!v) return SHF_HB_OK;
-  HB_TRY(hipMemset(c->d_status, 0, sizeof(v)));
-  return SHF_HB_ERR_ARG;
+  // read and clear in one atomic exchange on the device: a kernel on another
+  // stream that flags a key meanwhile leaves the word set for the next query
+  HB_TRY(shfhb::launch_status_take(c->d_status, c->d_status + 2, c->st[0]));
+  HB_TRY(hipMemcpyAsync(c->h_status, c->d_status + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, c->st[0]));
+  HB_TRY(hipStreamSynchronize(c->st[0]));
+  return *c->h_status ? SHF_HB_ERR_ARG : SHF_HB_OK;
 }
 
 int shf_hash_batch_device_count(void) { return visible_devices(); }

@@ -41,10 +41,7 @@ constexpr uint32_t kTabHdr = 24;                          // 6 x u32 (shf.privat
 constexpr uint32_t kTabRefs = 512 * 16;                   // SHF_ROWS_PER_TAB x SHF_REFS_PER_ROW
 constexpr uint32_t kTabData = kTabHdr + kTabRefs * 8;     // offsetof(SHF_TAB_MMAP, data) = 65560
 constexpr uint32_t kPage = 4096;                          // SHF_SIZE_PAGE
-#ifndef SHFHB_TAB_THREADS
-#define SHFHB_TAB_THREADS 512
-#endif
-constexpr uint32_t kThreads = SHFHB_TAB_THREADS;
+constexpr uint32_t kThreads = 512;  // one row per thread (1024 measured no faster)
 constexpr uint32_t kWaves = kThreads / 64;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -83,16 +80,10 @@ __device__ __forceinline__ void store_partial(uint8_t* p, u32x4 v, uint32_t n) {
   if (n & 1) p[o] = (uint8_t)lo;
 }
 
-#ifndef SHFHB_TAB_DPP_SCAN
-#define SHFHB_TAB_DPP_SCAN 1
-#endif
-
-// Wave-wide inclusive scan of a u32 (DPP variant: shifts by 1, 2, 4, 8 lanes
-// within each row of 16, then rows 0 and 1's last lanes added into the rows
-// after them; six VALU adds, no ds_bpermute).
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
-#if SHFHB_TAB_DPP_SCAN
-  (void)lane;
+// Wave-wide inclusive scan of a u32 (DPP: shifts by 1, 2, 4, 8 lanes within
+// each row of 16, then rows 0 and 1's last lanes added into the rows after
+// them; six VALU adds, no ds_bpermute; +7.5 % over a __shfl_up scan).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
@@ -100,14 +91,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
   return v;
-#else
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t u = (uint32_t)__shfl_up((int)v, d);
-    if (lane >= d) v += u;
-  }
-  return v;
-#endif
 }
 
 // One image's records in image order, in LDS: rank r at e[base + dir * r] (the
@@ -164,15 +147,7 @@ __device__ __forceinline__ void flag(shf_tab_job* job, int v) {
   *reinterpret_cast<volatile int32_t*>(&job->status) = v;
 }
 
-#ifndef SHFHB_TAB_POS_LENGTHS
-#define SHFHB_TAB_POS_LENGTHS 1
-#endif
-#ifndef SHFHB_TAB_EARLY_MOVE
-#define SHFHB_TAB_EARLY_MOVE 1
-#endif
-#ifndef SHFHB_TAB_CHUNKS
-#define SHFHB_TAB_CHUNKS 2  // 16-B chunks per lane in flight (2 and 4 within 5 %, 8 slower: profiles/r2/ab_tab)
-#endif
+constexpr uint32_t kChunksPerLane = 2;  // 16-B chunks per lane in flight (2 and 4 within 5 %, 8 slower: profiles/r2/ab_tab)
 
 // The first of L's n records whose end lies past x (n if none), x
 // wave-uniform: a 64-ary search, each round every lane probes one end and a
@@ -210,7 +185,7 @@ __device__ __forceinline__ unsigned __int128 put_at(unsigned __int128 out, unsig
 // Copy the image's data chunks [c_begin, c_end) (absolute 16-B chunks; the
 // image's data starts at absolute byte d0 and its records [0, nrec) are in L,
 // `total` bytes of them): consecutive chunks on consecutive lanes of the
-// workgroup, SHFHB_TAB_CHUNKS per lane in flight. A chunk takes its bytes from
+// workgroup, kChunksPerLane per lane in flight. A chunk takes its bytes from
 // the record holding its first byte and the next ones where it crosses a
 // record end, each loaded 16 B at the address that puts its bytes at their
 // chunk positions, then merged by byte masks (put_at); a record's first byte
@@ -227,7 +202,7 @@ __device__ __forceinline__ unsigned __int128 put_at(unsigned __int128 out, unsig
 __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList& L, uint32_t nrec, uint64_t total,
                             uint64_t d0, uint64_t c_begin, uint64_t c_end, uint32_t type, uint32_t t,
                             uint32_t* hist) {
-  constexpr uint32_t Q = SHFHB_TAB_CHUNKS;
+  constexpr uint32_t Q = kChunksPerLane;
   for (uint64_t base = c_begin; base < c_end; base += Q * kThreads) {
     unsigned __int128 v[Q];
     unsigned __int128 vn[Q];  // the next record's first bytes, for a chunk that crosses into it
@@ -251,7 +226,7 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
         const int64_t first = ((int64_t)e - a0 + 15) >> 4;
         if (e != 0xffffffffu && first < 64) atomicAdd(&hist[(uint32_t)first], 1u);
         __builtin_amdgcn_wave_barrier();
-        const uint32_t cnt = wave_incl_scan(hist[lane], lane);
+        const uint32_t cnt = wave_incl_scan(hist[lane]);
         __builtin_amdgcn_wave_barrier();
         if (cnt < 64u) l = h = r0 + cnt;
         else l = r0 + 64u;
@@ -304,46 +279,14 @@ __device__ void copy_chunks(const uint8_t* src, uint64_t src_len, const RecList&
 // copies its records while the lines those reads pulled in are still in L2 /
 // the Infinity Cache (one pass over the whole tab's lengths first would evict
 // them before the copy at 2 tabs per CU: the data are read twice from HBM).
-#ifndef SHFHB_TAB_SEGS
-#define SHFHB_TAB_SEGS 4
-#endif
-constexpr uint32_t kSegs = SHFHB_TAB_SEGS;
+constexpr uint32_t kSegs = 4;  // 2, 8 and 16 segments measured slower (profiles/r2/ab_tab)
 constexpr uint32_t kSegRefs = kTabRefs / kSegs;           // 2048
 constexpr uint32_t kSlabs = kSegRefs / kThreads;          // 4: ref = seg * 2048 + slab * 512 + thread
 
-// Phase stamps for profiling builds only (-DSHFHB_TAB_STAMPS=1, read back with
-// shf_tab_debug_stamps): thread 0 of each workgroup records the 100-MHz
-// real-time counter at fixed points, through ordinary vector stores.
-#ifndef SHFHB_TAB_STAMPS
-#define SHFHB_TAB_STAMPS 0
-#endif
-#if SHFHB_TAB_STAMPS
-constexpr uint32_t kStampWgs = 4096, kStamps = 16;
-__device__ uint64_t g_tab_stamps[kStampWgs * kStamps];
-#define TAB_STAMP(k)                                                                              \
-  do {                                                                                            \
-    if (threadIdx.x == 0 && blockIdx.x < kStampWgs)                                               \
-      g_tab_stamps[blockIdx.x * kStamps + (k)] = __builtin_amdgcn_s_memrealtime();                \
-  } while (0)
-#else
-#define TAB_STAMP(k) \
-  do {               \
-  } while (0)
-#endif
-
-#ifndef SHFHB_TAB_LDS_BARRIER
-#define SHFHB_TAB_LDS_BARRIER 1
-#endif
 // The segment loop's barriers guard LDS only (the scan sums, the record
 // lists, `bad`): wait for this wave's LDS accesses, not for its row and chunk
 // stores still in flight as __syncthreads() would (vmcnt(0)).
-__device__ __forceinline__ void seg_barrier() {
-#if SHFHB_TAB_LDS_BARRIER
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-  __syncthreads();
-#endif
-}
+__device__ __forceinline__ void seg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_tab_split(const uint8_t* __restrict__ src_base, uint64_t src_bytes,
                                                         uint8_t* dst_base, uint64_t dst_bytes, shf_tab_job* jobs,
@@ -354,10 +297,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ uint32_t wsum[2][kSlabs][4][kWaves];  // per segment parity, slab, quantity (keep/move bytes/refs), wave
   __shared__ int bad;
   __shared__ uint32_t max_len;  // the longest record copied (either image)
+  __shared__ unsigned long long len_total;  // every record length so far, exactly (u64)
   __shared__ uint32_t wtot[kWaves];
   __shared__ int slow;  // packed-tab fast path refused (workgroup-uniform after a barrier)
   __shared__ uint32_t whist[kWaves][64];  // copy_chunks' per-wave chunk histograms
-  TAB_STAMP(0);
   shf_tab_job* job = jobs + blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   const uint64_t src_len = job->src_len;
@@ -370,6 +313,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const uint64_t cap = job->cap;
   if (t == 0) {
     max_len = 0;
+    len_total = 0;
     // every byte a job names lies in its buffer; images are 8-B aligned
     bad = src_len < kTabData || job->src > src_bytes || src_len > src_bytes - job->src || cap < kTabData ||
           job->keep > dst_bytes || cap > dst_bytes - job->keep ||
@@ -401,7 +345,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   uint32_t lenreg[kSegs * kSlabs / 2];  // two u16 record lengths per word (longer records: no fast path)
   uint32_t mv_all = 0;                   // fast path, early move: bit seg * kSlabs + j = that ref moves
   bool fast = false;
-#if SHFHB_TAB_POS_LENGTHS
   if (!prm.fixed) {
     const uint32_t tab_used = load_u32(src + 4), data_free = load_u32(src + 16);  // shf.private.h:59-65
     if (data_free == 0 && tab_used >= kTabData && tab_used <= src_len && tab_used - kTabData < (1u << 30)) {
@@ -415,7 +358,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       if (t == 0) slow = 0;
       seg_barrier();
       uint32_t pk[kSegs * kSlabs], slot[kSegs * kSlabs];
-#if SHFHB_TAB_EARLY_MOVE
       uint32_t wk[kSegs * kSlabs];
 #pragma unroll
       for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
@@ -431,13 +373,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         for (uint32_t k = 0; k < kSegs * kSlabs; ++k)
           mv_all |= (uint32_t)(pk[k] != 0 && map[wk[k] & 0x7ffu] == tab_new) << k;
       }
-#else
-#pragma unroll
-      for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
-        const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
-        pk[k] = *reinterpret_cast<const uint32_t*>(src + kTabHdr + 8u * r + 4u);
-      }
-#endif
 #pragma unroll
       for (uint32_t k = 0; k < kSegs * kSlabs; ++k) {
         const uint32_t r = (k / kSlabs) * kSegRefs + (k % kSlabs) * kThreads + t;
@@ -452,7 +387,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         slot[k] = atomicAdd(&counts[(pk[k] - kTabData) / w], 1u);
       }
       seg_barrier();
-      TAB_STAMP(15);
       // exclusive scan of the bucket counts (thread t: buckets [t * kPer, t * kPer + kPer))
       uint32_t c[kPer], sum = 0;
 #pragma unroll
@@ -461,7 +395,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         sum += c[i];
         if (c[i] > 64u) slow = 1;  // insertion sort below stays short
       }
-      const uint32_t incl = wave_incl_scan(sum, lane);
+      const uint32_t incl = wave_incl_scan(sum);
       if (lane == 63) wtot[wave] = incl;
       seg_barrier();
       uint32_t before = 0, n_used = 0;
@@ -535,7 +469,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       // (the segment loop's first barrier orders these reads before the lists reuse the arrays)
     }
   }
-#endif
 
   for (uint32_t seg = 0; seg < kSegs; ++seg) {
     // 1. this thread's refs {tab:11 | rnd:21, pos} (shf.private.h:48-52) and their record lengths
@@ -560,20 +493,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       kl[j] = prm.fixed_key_len;
-      if (SHFHB_TAB_EARLY_MOVE && fast) continue;  // positions checked by the fast path's sort
+      if (fast) continue;  // positions checked by the fast path's sort
       if (!prm.fixed && pos[j] != 0) {
         if (pos[j] < kTabData || (uint64_t)pos[j] + 9u > src_len) mine_bad = true;
         else if (!fast) kl[j] = load_u32(src + pos[j] + 1);
       }
     }
     uint32_t to_move = 0;  // bit j: ref of slab j goes to the move image
-#if SHFHB_TAB_EARLY_MOVE
     if (fast) {  // lengths and images known; the refs just loaded are first needed by step 3
 #pragma unroll
       for (uint32_t j = 0; j < kSlabs; ++j) len[j] = lseg[j];
       to_move = (mv_all >> (seg * kSlabs)) & ((1u << kSlabs) - 1u);
     } else
-#endif
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       len[j] = 0;
@@ -597,12 +528,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
     if (mine_bad) bad = 1;
     {
+      // the longest record, and the exact u64 total of the lengths: the u32 scans
+      // below would wrap unnoticed on a corrupt image whose refs repeat one large
+      // record (each within the image, their sum not)
       uint32_t m = 0;
+      uint64_t sum = 0;
 #pragma unroll
-      for (uint32_t j = 0; j < kSlabs; ++j) m = max(m, len[j]);
+      for (uint32_t j = 0; j < kSlabs; ++j) {
+        m = max(m, len[j]);
+        sum += len[j];
+      }
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
-      if (lane == 0) atomicMax(&max_len, m);  // read after the segment loop's barriers
+      for (int d = 32; d >= 1; d >>= 1) {
+        m = max(m, (uint32_t)__shfl_xor((int)m, d));
+        sum += (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)sum, d) |
+               ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(sum >> 32), d) << 32);
+      }
+      if (lane == 0) {  // read after the segment loop's barriers
+        atomicMax(&max_len, m);
+        atomicAdd(&len_total, (unsigned long long)sum);
+      }
     }
 
     // 2. scans in ref order (slab by slab, thread by thread): in the wave, then over the waves
@@ -611,8 +556,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       const bool mv = (to_move >> j) & 1u;
-      const uint32_t ik = wave_incl_scan(mv ? 0u : len[j], lane), im = wave_incl_scan(mv ? len[j] : 0u, lane);
-      const uint32_t ic = wave_incl_scan(len[j] ? (mv ? 0x10000u : 1u) : 0u, lane);
+      const uint32_t ik = wave_incl_scan(mv ? 0u : len[j]), im = wave_incl_scan(mv ? len[j] : 0u);
+      const uint32_t ic = wave_incl_scan(len[j] ? (mv ? 0x10000u : 1u) : 0u);
       if (lane == 63) {
         wsum[seg & 1][j][0][wave] = ik;
         wsum[seg & 1][j][1][wave] = im;
@@ -620,15 +565,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       }
     }
     seg_barrier();
-    TAB_STAMP(1 + 3 * seg);
     uint64_t seg_k = 0, seg_m = 0;  // this segment's keep and move bytes so far
     uint32_t seg_c = 0;             // and records (packed: keep low, move high half)
     // 3. each ref's record offset in its image, its list entry, its row entry in both images
 #pragma unroll
     for (uint32_t j = 0; j < kSlabs; ++j) {
       const bool mv = (to_move >> j) & 1u, used = len[j] != 0;
-      const uint32_t ik = wave_incl_scan(mv ? 0u : len[j], lane), im = wave_incl_scan(mv ? len[j] : 0u, lane);
-      const uint32_t ic = wave_incl_scan(used ? (mv ? 0x10000u : 1u) : 0u, lane);
+      const uint32_t ik = wave_incl_scan(mv ? 0u : len[j]), im = wave_incl_scan(mv ? len[j] : 0u);
+      const uint32_t ic = wave_incl_scan(used ? (mv ? 0x10000u : 1u) : 0u);
       uint32_t bk = 0, bm = 0, bc = 0, ak = 0, am = 0, ac = 0;  // before this wave / whole slab
 #pragma unroll
       for (uint32_t w = 0; w < kWaves; ++w) {
@@ -665,10 +609,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     refs_keep += (uint32_t)seg_tot[2];
     refs_move += (uint32_t)seg_tot[3];
     if (t == 0 && (kTabData + done_keep > cap || (moving && kTabData + done_move > cap) ||
-                   kTabData + done_keep + done_move > 0xffffffffull))
+                   kTabData + done_keep + done_move > 0xffffffffull || kTabData + len_total > 0xffffffffull))
       bad = 1;
     seg_barrier();
-    TAB_STAMP(2 + 3 * seg);
     if (bad) break;  // workgroup-uniform; nothing past cap was or will be written
 
     // 4. the data chunks this segment completes (every byte below done_*)
@@ -679,7 +622,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, end_m, move_type, t, whist[wave]);
       next_m = end_m;
     }
-    TAB_STAMP(3 + 3 * seg);
   }
   if (bad) {
     if (t == 0) flag(job, SHF_HB_ERR_ARG);
@@ -688,7 +630,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // the last partial chunk of each image
   copy_chunks(src, src_len, LK, refs_keep, done_keep, d0k, next_k, (d0k + done_keep + 15u) >> 4, keep_type, t, whist[wave]);
   if (moving) copy_chunks(src, src_len, LM, refs_move, done_move, d0m, next_m, (d0m + done_move + 15u) >> 4, move_type, t, whist[wave]);
-  TAB_STAMP(13);
 
   // 5. headers: tab_size (replayed growth), tab_used, tab_refs_used (SHF_TAB_APPEND and
   //    SHF_TAB_REF_COPY both count each copied ref, shf.c:608, :651), free pos, free, data used
@@ -712,16 +653,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       store_u32(img + 20, (uint32_t)total);
     }
   }
-  TAB_STAMP(14);
   if (t == 0) flag(job, SHF_HB_OK);
 }
 
-#if SHFHB_TAB_STAMPS
-int tab_debug_stamps(uint64_t* out, uint64_t n) {
-  if (n > (uint64_t)kStampWgs * kStamps) n = (uint64_t)kStampWgs * kStamps;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tab_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint64_t dst_bytes, shf_tab_job* jobs,
                             uint32_t n_jobs, const uint16_t* maps, uint32_t n_maps, const shf_tab_params& prm,
@@ -734,8 +668,3 @@ hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint
 
 }  // namespace shfhb
 
-#if SHFHB_TAB_STAMPS
-extern "C" __attribute__((visibility("default"))) int shf_tab_debug_stamps(uint64_t* out, uint64_t n) {
-  return shfhb::tab_debug_stamps(out, n);
-}
-#endif

@@ -23,6 +23,7 @@
  * GPU (the library refused: no CPU fallback).
  */
 #define _GNU_SOURCE
+#include <ftw.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,6 +49,14 @@ static int fail(const char *what)
 {
     fprintf(stderr, "test_seam: FAIL: %s\n", what);
     return 1;
+}
+
+static int remove_entry(const char *path, const struct stat *sb, int flag, struct FTW *ftw)
+{
+    (void)sb;
+    (void)flag;
+    (void)ftw;
+    return remove(path);
 }
 
 static uint64_t good_values;
@@ -172,8 +181,9 @@ int main(int argc, char **argv)
            (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
            (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
            (unsigned long long)ffound);
-    (void)shf_del(shf);
-    (void)shf_del(fshf);
-    rmdir(folder);
+    /* the stores' files go with the folder (shf_del would run `du` and `rm` through popen) */
+    shf_detach(shf);
+    shf_detach(fshf);
+    nftw(folder, remove_entry, 16, FTW_DEPTH | FTW_PHYS);
     return 0;
 }

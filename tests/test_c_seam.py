@@ -64,3 +64,48 @@ def test_seam_program_put_and_probed_get():
     assert r["ref_found"] == r["n_put"] == r["ref_right"] == r["probed_found"] == 200000
     assert r["probed_fast"] > 0.9 * r["n_put"]
     assert r["fixed_found"] == 50000
+
+
+# ---- the C++ seam: include/shf_hash_batch_shf.hpp through the reference's SharedHashFile class ----
+BIN_CPP = os.path.join(ROOT, "tests", "c", "build", "test_seam_cpp")
+
+
+def test_cpp_seam_header_compiles_against_reference_class():
+    if not os.path.isdir("/root/reference/src"):
+        pytest.skip("reference headers absent")
+    src = ('#include "SharedHashFile.hpp"\n#include "shf_hash_batch_shf.hpp"\n'
+           'int main(){ shf_hash128 h = {1, 2}; shf_hash_batch::UseHash("k", 1, h);'
+           ' return shf_hash.u64[1] == 2 && shf_hash_key_len == 1 ? 0 : 1; }\n')
+    p = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                        "-I", "/root/reference/src", "-x", "c++", "-"], input=src.encode(), capture_output=True)
+    assert p.returncode == 0, p.stderr.decode()
+
+
+def test_cpp_seam_header_refuses_without_reference_class():
+    src = '#include "shf_hash_batch_shf.hpp"\nint main(){return 0;}\n'
+    p = subprocess.run(["g++", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), "-x", "c++", "-"],
+                       input=src.encode(), capture_output=True)
+    assert p.returncode != 0 and b"SharedHashFile.hpp" in p.stderr
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device behaviour")
+def test_cpp_seam_program_fails_loudly_without_gpu():
+    if not os.path.exists(BIN_CPP):
+        pytest.skip("tests/c/build/test_seam_cpp not built (needs /root/reference headers at build time)")
+    p = subprocess.run([BIN_CPP, "1000"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2, (p.returncode, p.stderr)
+    assert "no usable GPU" in p.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_seam_program_own_hash_block_and_put_batch():
+    """test.a.shf.cpp:172-270's own-hash block with GPU batch hashes, PutBatch
+    through the class and the reference's MakeHash get, fixed 16-B keys."""
+    if not os.path.exists(BIN_CPP):
+        pytest.skip("tests/c/build/test_seam_cpp not built (needs /root/reference headers at build time)")
+    p = subprocess.run([BIN_CPP, "100000"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["failures"] == 0 and r["checks"] == 4 * 9 + 6
+    assert r["found"] == r["right"] == r["n_put"] == 100000 and r["absent_found"] == 0
+    assert r["fixed_found"] == 50000
