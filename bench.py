@@ -23,6 +23,16 @@ Every line: min / median / max over --repeats timed repeats of K steps each
 of the timed batches are checked against the CPU oracle (the checker only;
 `verified`).
 
+Ceilings measured in the same run on the same box (`secondary.ceil_*`,
+include/shf_hash_batch_ceiling.h): a 16-B/lane copy in k_fixed16's launch shape
+on the headline's own rotating buffers (and on the hot batch and the 1B-key
+buffers), a 16:1 read-mostly copy on configs[2]'s buffers, the probe's 128-B
+row gather and an unaligned 16-B stream. Every `roofline.frac_of_copy_ceiling`
+divides by the ceiling of the matching shape measured here, never by a
+constant; the gathers and the unaligned stream also calibrate rocprofv3's
+FETCH_SIZE for the probe and the tab copy, and two VALU-saturating launches
+calibrate the VALUBusy formula (`valu_busy`).
+
 Multi-GPU: one process per GPU, each hashes its own
 independent shard (no collective on the data path; torch.distributed is used
 only for the start/stop barriers and the max over ranks of the elapsed time).
@@ -51,7 +61,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "keys hashed/s device-resident (16 B & 256 B keys) + GiB/s vs HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E peak (spec)
-HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: best measured float4 copy
 SIMDS = 256 * 4        # 256 CUs x 4 SIMDs
 XCDS = 8
 SEED = 12345
@@ -59,14 +68,29 @@ WARMUP_MIN_S = 0.25  # untimed warmup floor per workload (seconds of GPU work)
 VERIFY_SAMPLES = 20_000
 BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for worker pools)
 
-# rocprofv3 kernel-name substrings of each workload's kernel (PMC passes)
+# rocprofv3 kernel-name substrings of each workload's kernel (PMC passes; rows
+# are also matched on the launch's grid size, Workload.grid)
 KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
                "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>",
-               "tabpart": "k_tab_split"}
-# kernels whose reads are not 16-B-per-lane streams: FETCH_SIZE's x2 (calibrated for those only,
-# MI355X_MICROARCH.md "HBM") is not known to hold, so their traffic is reported raw beside it
-FETCH_UNCALIBRATED = {"probe16": "128-B row gathers (8 lanes x 16 B) and 4-B tab-map lookups",
-                      "tabpart": "8-B ref loads and byte/dword record gathers"}
+               "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy", "ceil_copy_hot": "k_ceil_copy",
+               "ceil_copy_1b": "k_ceil_copy", "ceil_read16": "k_ceil_read16", "ceil_gather128": "k_ceil_gather128",
+               "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
+               "ceil_valu_mul": "k_ceil_valu<1>"}
+HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart"]
+CEIL_WORKLOADS = ["ceil_copy", "ceil_copy_hot", "ceil_copy_1b", "ceil_read16", "ceil_gather128", "ceil_stream16u",
+                  "ceil_valu_add", "ceil_valu_mul"]
+# the ceiling each hashing line is reported against: the copy of the same shape on the same buffers
+CEILING_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy_hot", "shard1b": "ceil_copy_1b",
+              "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128", "tabpart": "ceil_copy"}
+# the pattern whose known byte count calibrates each line's FETCH_SIZE
+FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
+                "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
+                "tabpart": "ceil_stream16u"}
+# bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
+CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copy_hot": 16, "ceil_copy_1b": 16, "ceil_read16": 256,
+                      "ceil_gather128": 132, "ceil_stream16u": 16}
+VALU_ITERS = 2048          # rounds of 8 chained VALU ops per lane in the VALU-saturating launches
+VALU_LANES = 256 * 32 * 64  # 32 waves per CU on 256 CUs
 
 
 def parse(argv=None):
@@ -81,10 +105,11 @@ def parse(argv=None):
                    help="configs[4]: 16-B keys for the whole job, split over the GPUs (strong scaling)")
     p.add_argument("--keys256", type=int, default=100_000_000, help="configs[2]: 256-B keys per GPU")
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
-    p.add_argument("--only", default="", help="comma list of fixed16,fixed16_hot,shard1b,fixed256,var,probe16,tabpart")
+    p.add_argument("--only", default="", help="comma list of %s, %s" % (",".join(HASH_WORKLOADS),
+                                                                           ",".join(CEIL_WORKLOADS)))
     p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
     p.add_argument("--tab-jobs", type=int, default=1024, help="tabpart: tabs parted per step (f4)")
-    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "generic", "round"])
+    p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "span_pp", "generic", "round"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -96,8 +121,9 @@ def parse(argv=None):
     p.add_argument("--host-keys", type=int, default=10_000_000, help="keys per host-inclusive batch")
     p.add_argument("--allow-shared-gpu", action="store_true",
                    help="rehearsal only: let ranks share GPUs (gloo barriers; the line is marked rehearsal)")
-    p.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
-                   help="backend for the barriers / max-reduce only (auto: nccl, gloo when GPUs are shared)")
+    p.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"],
+                   help="backend of the start/stop barriers and the max-over-ranks reduce only (no data crosses "
+                        "GPUs): gloo on CPU tensors by default, RCCL on request")
     p.add_argument("--warmup-min-s", type=float, default=WARMUP_MIN_S,
                    help="keep warming up (untimed) until this many seconds of the workload have run")
     p.add_argument("--quiet", action="store_true")
@@ -142,17 +168,20 @@ def _free_port():
     return port
 
 
+def rank_envs(n, port, base=None):
+    """The environment of each of n rank processes on this node (one GPU each)."""
+    base = dict(os.environ if base is None else base)
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(n)]
+
+
 def launch_ranks(argv, n):
     """Start n rank processes of this script (RANK/WORLD_SIZE/... in their
     environment) and wait for them. This process never touches the GPU: the
     ranks are children, not an exec of a GPU-initialised process. The first
     rank to fail stops the others (by PID)."""
-    port = _free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env)
+             for env in rank_envs(n, _free_port())]
     rc = 0
     while procs:
         for p in list(procs):
@@ -175,9 +204,10 @@ class Workload:
     """Device-resident batches and the launch that hashes one of them.
     launch(i) hashes batch i % len(batches) into its own output."""
 
-    def __init__(self, name, n, bytes_per_key, launches, kernel, desc, verify=None):
+    def __init__(self, name, n, bytes_per_key, launches, kernel, desc, verify=None, grid=None):
         self.name, self.n, self.bytes_per_key = name, n, bytes_per_key
         self.launches, self.kernel, self.desc, self.verify = launches, kernel, desc, verify
+        self.grid = grid  # work-items of one launch of the measured kernel (matches rocprofv3's Grid_Size)
         self.job_keys = None
 
     def launch(self, i):
@@ -252,36 +282,84 @@ def verify_var(data, off, out, samples, seed):
     return bool(np.array_equal(got, Oracle().hash_var(sub, hoff))), int(idx.size)
 
 
+def _up(x, m):
+    return (x + m - 1) // m * m
+
+
+def grid_threads(name, n):
+    """Work-items of one launch of workload `name` over n keys / lanes / jobs:
+    rocprofv3's Grid_Size of that launch (the PMC rows are matched on it)."""
+    if name in ("fixed16", "fixed16_hot", "shard1b", "probe16") or name.startswith("ceil_"):
+        return _up(n, 256)              # 256-thread blocks, one key / lane per thread
+    if name == "fixed256":
+        return _up(n, 64)               # k_tiled: one 64-thread workgroup per 64-key tile
+    if name == "var":
+        return ((n + 63) // 64 + 1) // 2 * 128  # k_span_pp: one 128-thread workgroup per two tiles
+    if name == "tabpart":
+        return n * 512                  # k_tab_split: one 512-thread workgroup per tab
+    return None
+
+
+def read16_lanes(args, only):
+    """Lanes of the read-mostly ceiling: configs[2]'s keys when that line runs (its own buffers), else 10M."""
+    n = args.keys256 if "fixed256" in only else min(args.keys256, 10_000_000)
+    return n - n % 64
+
+
+def ceil_launcher(hb, kind, src, src_bytes, idx, dst, n, dev):
+    """shf_hb_ceiling_async (include/shf_hash_batch_ceiling.h) with its ctypes arguments built once."""
+    import ctypes
+
+    import torch
+
+    fn = hb.load().shf_hb_ceiling_async
+    argv = (ctypes.c_int(kind), ctypes.c_void_p(src), ctypes.c_uint64(src_bytes), ctypes.c_void_p(idx or 0),
+            ctypes.c_void_p(dst), ctypes.c_uint64(n), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+
+    def launch():
+        rc = fn(*argv)
+        if rc:
+            raise hb.ShfHashBatchError(rc, "shf_hb_ceiling_async(%d)" % kind)
+
+    return launch
+
+
 def make_workloads(args, dev, rank, world=1):
     import torch
 
     import sharedhashfile_amd as hb
     from sharedhashfile_amd.keygen import device_random_bytes
 
-    only = set(filter(None, args.only.split(","))) or {"fixed16", "fixed16_hot", "shard1b", "fixed256", "var",
-                                                        "probe16", "tabpart"}
+    only = set(filter(None, args.only.split(","))) or set(HASH_WORKLOADS + CEIL_WORKLOADS)
     wl = []
     seed_base = 0x5348460000000001 + 1000 * rank
     fk16 = {"auto": 0, "fixed16": 1, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
+    bufs = {}
+
+    def fixed16_pairs():  # configs[1]'s rotating batches (keys + outputs), shared by its copy ceiling
+        if "pairs" not in bufs:
+            n = args.keys16
+            bufs["pairs"] = [(device_random_bytes(n * 16, seed_base + 1 + 100 * b, dev),
+                              torch.empty((n, 2), dtype=torch.int64, device=dev)) for b in range(max(1, args.rotate))]
+        return bufs["pairs"]
+
     if "fixed16" in only or "fixed16_hot" in only:
         n = args.keys16
-        B = max(1, args.rotate)
-        pairs = []
-        for b in range(B):
-            keys = device_random_bytes(n * 16, seed_base + 1 + 100 * b, dev)
-            pairs.append((keys, torch.empty((n, 2), dtype=torch.int64, device=dev)))
+        pairs = fixed16_pairs()
+        B = len(pairs)
         if "fixed16" in only:
             wl.append(Workload("fixed16", n, 16 + 16, [fast_launch(hb, k, 16, n, o, fk16, dev) for k, o in pairs],
                                "k_fixed16", "%d fixed 16-B keys per step, rotating over %d distinct batches "
                                "(%.2f GB of keys + hashes)" % (n, B, B * n * 32 / 1e9),
-                               lambda p=pairs: verify_fixed(p, 16, VERIFY_SAMPLES, 11)))
+                               lambda p=pairs: verify_fixed(p, 16, VERIFY_SAMPLES, 11), grid_threads("fixed16", n)))
         if "fixed16_hot" in only:
             k0, o0 = pairs[0]
             wl.append(Workload("fixed16_hot", n, 16 + 16, [fast_launch(hb, k0, 16, n, o0, fk16, dev)], "k_fixed16",
                                "%d fixed 16-B keys, the same batch every step (its 320 MB partly stay in the "
                                "256 MiB Infinity Cache)" % n,
-                               lambda p=pairs[:1]: verify_fixed(p, 16, VERIFY_SAMPLES, 12)))
-    if "shard1b" in only:
+                               lambda p=pairs[:1]: verify_fixed(p, 16, VERIFY_SAMPLES, 12),
+                               grid_threads("fixed16_hot", n)))
+    if "shard1b" in only or "ceil_copy_1b" in only:
         # configs[4]: 1B 16-B keys split evenly over the job's GPUs (strong scaling:
         # 1B / world keys on this rank, contiguous index range, no collective).
         from sharedhashfile_amd.shard import shard_range
@@ -291,20 +369,24 @@ def make_workloads(args, dev, rank, world=1):
         n = hi - lo
         keys = device_random_bytes(n * 16, seed_base + 6, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
-        w = Workload("shard1b", n, 16 + 16, [fast_launch(hb, keys, 16, n, out, 0, dev)], "k_fixed16",
-                     "%d 16-B keys split over %d rank(s): keys [%d, %d) on rank %d" % (total, world, lo, hi, rank),
-                     lambda p=[(keys, out)]: verify_fixed(p, 16, VERIFY_SAMPLES, 13))
-        w.job_keys = total
-        w.shard = (lo, hi)
-        wl.append(w)
+        bufs["shard1b"] = (keys, out, n)
+        if "shard1b" in only:
+            w = Workload("shard1b", n, 16 + 16, [fast_launch(hb, keys, 16, n, out, 0, dev)], "k_fixed16",
+                         "%d 16-B keys split over %d rank(s): keys [%d, %d) on rank %d" % (total, world, lo, hi, rank),
+                         lambda p=[(keys, out)]: verify_fixed(p, 16, VERIFY_SAMPLES, 13), grid_threads("shard1b", n))
+            w.job_keys = total
+            w.shard = (lo, hi)
+            wl.append(w)
     if "fixed256" in only:
         n = args.keys256
         keys = device_random_bytes(n * 256, seed_base + 2, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        bufs["fixed256"] = (keys, out, n)
         fk = {"auto": 0, "fixed16": 2, "tiled": 2, "generic": 3, "span": 4}[args.fixed_kernel]
         wl.append(Workload("fixed256", n, 256 + 16, [fast_launch(hb, keys, 256, n, out, fk, dev)],
                            "k_tiled", "%d fixed 256-B keys" % n,
-                           lambda p=[(keys, out)]: verify_fixed(p, 256, VERIFY_SAMPLES, 14)))
+                           lambda p=[(keys, out)]: verify_fixed(p, 256, VERIFY_SAMPLES, 14),
+                           grid_threads("fixed256", n)))
     if "var" in only:
         n = args.keysvar
         g = torch.Generator(device=dev)
@@ -316,13 +398,14 @@ def make_workloads(args, dev, rank, world=1):
         data = device_random_bytes(total, seed_base + 4, dev)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         del lens
-        vk = {"auto": 0, "span": 4, "generic": 3, "round": 5}[args.var_kernel]
+        vk = {"auto": 0, "span": 4, "span_pp": 6, "generic": 3, "round": 5}[args.var_kernel]
         wl.append(Workload("var", n, total / n + 8 + 16,
                            [lambda d=data, o=off, out=out, vk=vk, tb=total: hb.hash_var(d, o, out=out, kernel=vk, key_bytes=tb)],
-                           {"generic": "k_generic", "round": "k_vround", "span": "k_span_pp"}.get(args.var_kernel,
-                                                                                                  "k_span_pp"),
+                           {"generic": "k_generic", "round": "k_vround", "span": "k_span"}.get(args.var_kernel,
+                                                                                               "k_span_pp"),
                            "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9),
-                           lambda d=data, o=off, out=out: verify_var(d, o, out, VERIFY_SAMPLES, 15)))
+                           lambda d=data, o=off, out=out: verify_var(d, o, out, VERIFY_SAMPLES, 15),
+                           grid_threads("var", n) if args.var_kernel in ("auto", "span_pp") else None))
     if "probe16" in only:
         # Row pre-probe: hash + row scan of every key against an index holding
         # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +
@@ -354,12 +437,99 @@ def make_workloads(args, dev, rank, world=1):
         w = Workload("probe16", n, 16 + 128 + 16 + 4 * 256 * 2048 / n,
                      [lambda k=keys, o=out, ix=index: hb.probe_fixed(ix, k, 16, out=o)],
                      "k_fixed16<kOutProbe>", "%d fixed 16-B keys hashed and probed against a row index of "
-                     "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed), verify_probe)
+                     "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed), verify_probe,
+                     grid_threads("probe16", n))
         w.index = index
         wl.append(w)
     if "tabpart" in only:
         wl.append(tab_workload(args, dev, seed_base))
+    wl += ceiling_workloads(args, dev, only, bufs, fixed16_pairs)
     torch.cuda.synchronize()
+    return wl
+
+
+def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
+    """The on-box ceilings (include/shf_hash_batch_ceiling.h), each on the
+    buffers of the hashing line it bounds. `n` counts lanes; bytes_per_key is
+    what one lane moves."""
+    import torch
+
+    import sharedhashfile_amd as hb
+
+    wl = []
+    if "ceil_copy" in only or "ceil_copy_hot" in only:
+        pairs = fixed16_pairs()
+        n = args.keys16
+        if "ceil_copy" in only:
+            wl.append(Workload("ceil_copy", n, 32,
+                               [ceil_launcher(hb, hb.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
+                                for k, o in pairs], "k_ceil_copy",
+                               "16-B/lane copy in k_fixed16's shape over fixed16's %d rotating batches" % len(pairs),
+                               grid=grid_threads("ceil_copy", n)))
+        if "ceil_copy_hot" in only:
+            k, o = pairs[0]
+            wl.append(Workload("ceil_copy_hot", n, 32,
+                               [ceil_launcher(hb, hb.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
+                               "k_ceil_copy", "the same copy over fixed16_hot's single batch",
+                               grid=grid_threads("ceil_copy_hot", n)))
+    if "ceil_copy_1b" in only:
+        keys, out, n = bufs["shard1b"]
+        wl.append(Workload("ceil_copy_1b", n, 32,
+                           [ceil_launcher(hb, hb.CEIL_COPY, keys.data_ptr(), 16 * n, None, out.data_ptr(), n, dev)],
+                           "k_ceil_copy", "the same copy over shard1b's %d keys + hashes" % n,
+                           grid=grid_threads("ceil_copy_1b", n)))
+    if "ceil_read16" in only:
+        n = read16_lanes(args, only)
+        if "fixed256" in bufs:
+            keys, out, _ = bufs["fixed256"]
+            where = "fixed256's keys and hashes"
+        else:
+            keys = torch.empty(n * 256, dtype=torch.uint8, device=dev)
+            out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+            where = "a buffer of its own"
+        wl.append(Workload("ceil_read16", n, 272,
+                           [ceil_launcher(hb, hb.CEIL_READ16, keys.data_ptr(), 256 * n, None, out.data_ptr(), n,
+                                          dev)], "k_ceil_read16",
+                           "16:1 read-mostly copy (16 x 16 B nt loads per lane, one contiguous 16 KiB per wave, "
+                           "16-B store) over %s, %d lanes" % (where, n), grid=grid_threads("ceil_read16", n)))
+        wl[-1].keep = (keys, out)
+    if "ceil_gather128" in only:
+        n = args.keys16
+        rows = torch.empty(n * 128, dtype=torch.uint8, device=dev)
+        idx = torch.randperm(n, device=dev, dtype=torch.int32)
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        wl.append(Workload("ceil_gather128", n, 148,
+                           [ceil_launcher(hb, hb.CEIL_GATHER128, rows.data_ptr(), rows.numel(), idx.data_ptr(),
+                                          out.data_ptr(), n, dev)], "k_ceil_gather128",
+                           "each of %d 128-B rows read once in random order, 8 lanes per row (the probe's row fetch) "
+                           "+ 4-B index + 16-B store per lane" % n, grid=grid_threads("ceil_gather128", n)))
+        wl[-1].keep = (rows, idx, out)
+    if "ceil_stream16u" in only:
+        n = 2 * args.keys16
+        bs = [(torch.empty(16 * n + 16, dtype=torch.uint8, device=dev), torch.empty((n, 2), dtype=torch.int64,
+                                                                                    device=dev)) for _ in range(2)]
+        wl.append(Workload("ceil_stream16u", n, 32,
+                           [ceil_launcher(hb, hb.CEIL_STREAM16U, s_.data_ptr(), s_.numel(), None, o.data_ptr(), n, dev)
+                            for s_, o in bs], "k_ceil_stream16u",
+                           "16-B loads 7 bytes off alignment (the tab copy's record loads) + 16-B stores, %d lanes, "
+                           "2 rotating buffers" % n, grid=grid_threads("ceil_stream16u", n)))
+        wl[-1].keep = bs
+    for name, kind in (("ceil_valu_add", hb.CEIL_VALU_ADD), ("ceil_valu_mul", hb.CEIL_VALU_MUL)):
+        if name not in only:
+            continue
+        out = torch.empty((VALU_LANES, 2), dtype=torch.int64, device=dev)
+        w = Workload(name, VALU_LANES, 16, [ceil_launcher(hb, kind, 1, VALU_ITERS, None, out.data_ptr(), VALU_LANES,
+                                                          dev)], "k_ceil_valu",
+                     "VALU-saturating launch: 8 independent %s chains x %d rounds per lane, %d lanes (32 waves/CU)"
+                     % ("v_add_u32" if kind == hb.CEIL_VALU_ADD else "v_mul_lo_u32", VALU_ITERS, VALU_LANES),
+                     grid=grid_threads(name, VALU_LANES))
+        w.unit = "VALU lane-ops/s"
+        w.ops_per_key = 8 * VALU_ITERS
+        w.keep = out
+        wl.append(w)
+    for w in wl:
+        if not hasattr(w, "unit"):
+            w.unit = "lanes/s"
     return wl
 
 
@@ -437,7 +607,8 @@ def tab_workload(args, dev, seed_base):
     w = Workload("tabpart", J, per_job, [launch], "k_tab_split",
                  "%d tab parts per step (f4: shf_tab_part's copy, both output tabs), synthetic tabs of 4500 refs "
                  "with %.2f MB of records each, %.2f GB moved per step" % (
-                     J, float(np.mean([img.size - 65560 for img, _, _ in base])) / 1e6, J * per_job / 1e9), verify)
+                     J, float(np.mean([img.size - 65560 for img, _, _ in base])) / 1e6, J * per_job / 1e9), verify,
+                 grid_threads("tabpart", J))
     w.unit = "tabs/s"
     w.keep = (src, dst, d_jobs, d_maps, prm)
     return w
@@ -445,7 +616,8 @@ def tab_workload(args, dev, seed_base):
 
 def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP_MIN_S):
     """Per repeat: (wall seconds for `steps` steps, max over ranks; mean per-launch
-    device seconds from HIP events on the launch stream, max over ranks)."""
+    device seconds from HIP events on the launch stream, max over ranks; the
+    same, this rank's own)."""
     import torch
 
     stream = torch.cuda.current_stream()  # the stream every launch goes to (hb passes it to the library)
@@ -481,6 +653,7 @@ def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP
         # time per launch, back-to-back kernels (inter-kernel gaps included)
         devs.append(ev0.elapsed_time(ev1) / steps / 1e3)
         enq.append(t_enq - t0)
+    devs_local = list(devs)
     if dist:
         import torch as _t
 
@@ -488,7 +661,7 @@ def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         walls, devs = [float(x) for x in t[:repeats]], [float(x) for x in t[repeats:]]
     w.enqueue_s = float(np.median(enq))
-    return walls, devs
+    return walls, devs, devs_local
 
 
 # ---------------------------------------------------------------------------
@@ -655,8 +828,7 @@ def cpu_baseline(args):
            "host_cpus": cpus}
     # SURVEY.md s8(d) config A also asks for the host's cores. This box's rule
     # sizes host worker pools to its CPU share per GPU (16 threads): that leg is
-    # measured; the whole host (`visible` CPUs) is extrapolated from the
-    # per-thread rate of that leg, never measured here, and labelled so.
+    # measured (the whole host's CPUs are not this job's to use).
     threads = min(BOX_CPU_SHARE, cpus["affinity"])
     if threads > 1:
         mt_passes = max(1, int(passes * threads / 4))  # ~1/4 of the single-thread time if it scales
@@ -665,80 +837,142 @@ def cpu_baseline(args):
         out["threads%d" % threads] = {"value": v, "unit": "keys/s", "cores": threads,
                                       "sample": "%d passes x 1M 16-B keys over %d threads (even key ranges), %.1f s"
                                                 % (mt_passes, threads, dt_mt)}
-        out["all_visible_cpus_extrapolated"] = {
-            "value": v / threads * cpus["visible"], "unit": "keys/s", "cores": cpus["visible"], "measured": False,
-            "sample": "the %d-thread rate per thread x %d visible CPUs (linear scaling assumed; not run: the GPU box "
-                      "limits a job's host worker pools to its %d-CPU share)" % (threads, cpus["visible"],
-                                                                                BOX_CPU_SHARE)}
     return out
 
 
 # ---------------------------------------------------------------------------
-# rocprofv3 PMC passes (child processes, N=1 only): HBM bytes and VALU busy
+# rocprofv3 PMC passes (child processes, N=1 only): HBM bytes, VALU, waits
 # ---------------------------------------------------------------------------
 PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"],
-              ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"]]
+              ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+               "GRBM_GUI_ACTIVE"]]
+PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b")  # same kernels and grids as measured ones
+
+
+def pmc_child_sizes(args, want):
+    """Lanes / keys / jobs of each workload in the PMC child (configs 2 and 3
+    at <= 10M keys: their per-key figures do not depend on the batch size)."""
+    k256, kvar = min(args.keys256, 10_000_000), min(args.keysvar, 10_000_000)
+    child = argparse.Namespace(keys256=k256, keys16=args.keys16)
+    sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
+             "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_read16": read16_lanes(child, set(want)),
+             "ceil_gather128": args.keys16, "ceil_stream16u": 2 * args.keys16, "ceil_valu_add": VALU_LANES,
+             "ceil_valu_mul": VALU_LANES}
+    return {w: sizes[w] for w in want if w in sizes}, k256, kvar
+
+
+def parse_pmc_rows(rows, grids):
+    """{workload: {counter: [values]}} from rocprofv3 counter_collection rows:
+    a row counts for a workload when its kernel name holds the workload's
+    symbol and its grid is the workload's launch grid."""
+    vals = {}
+    for row in rows:
+        name = row.get("Kernel_Name", "")
+        try:
+            grid = int(float(row.get("Grid_Size") or -1))
+        except ValueError:
+            grid = -1
+        for w, g in grids.items():
+            if KERNEL_SYMS[w] in name and (g is None or grid < 0 or grid == g):
+                vals.setdefault(w, {}).setdefault(row.get("Counter_Name"), []).append(float(row["Counter_Value"]))
+    return vals
 
 
 def collect_pmc(args, names):
     """One rocprofv3 --pmc pass per counter group over a short child bench of
-    the given workloads (the 16-B workloads at the headline size; configs 2
-    and 3 at 10M keys, whose per-key figures do not depend on the batch size).
-    Returns ({workload: {counter: median per launch}}, note)."""
+    the given workloads. Returns ({workload: {counter: median per launch,
+    "_lanes": n in the child}}, note)."""
     prof = shutil.which("rocprofv3")
     if not prof:
         return None, "rocprofv3 not found"
-    want = [x for x in names if x in KERNEL_SYMS and x not in ("fixed16_hot", "shard1b")]
-    res = {w: {} for w in want}
+    want = [x for x in names if x in KERNEL_SYMS and x not in PMC_SKIP]
+    sizes, k256, kvar = pmc_child_sizes(args, want)
+    grids = {w: grid_threads(w, sizes[w]) for w in want}
+    if args.var_kernel not in ("auto", "span_pp"):
+        grids.pop("var", None)
+        want = [w for w in want if w != "var"]
+    res = {w: {"_lanes": sizes[w]} for w in want}
     for group in PMC_PASSES:
         outdir = tempfile.mkdtemp(prefix="shfhb_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [prof, "--pmc"] + group + ["--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
                                          sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup",
                                          "1", "--repeats", "1", "--only", ",".join(want), "--no-cpu", "--no-verify",
                                          "--no-host-inclusive", "--traffic", "off", "--quiet", "--keys16",
-                                         str(args.keys16), "--keys256", str(min(args.keys256, 10_000_000)),
-                                         "--keysvar", str(min(args.keysvar, 10_000_000)), "--warmup-min-s", "0",
-                                         "--gpus", "1"]
+                                         str(args.keys16), "--keys256", str(k256), "--keysvar", str(kvar),
+                                         "--tab-jobs", str(args.tab_jobs), "--warmup-min-s", "0", "--gpus", "1",
+                                         "--fixed-kernel", args.fixed_kernel, "--var-kernel", args.var_kernel]
         try:
             subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            cwd=os.environ.get("TMPDIR", "/tmp"))
         except Exception as e:  # noqa: BLE001
             shutil.rmtree(outdir, ignore_errors=True)
             return None, "rocprofv3 --pmc %s failed: %s" % (" ".join(group), e)
-        vals = {}
+        rows = []
         for f in glob.glob(os.path.join(outdir, "**", "*counter_collection*.csv"), recursive=True):
             with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    for w in want:
-                        if KERNEL_SYMS[w] in row.get("Kernel_Name", ""):
-                            vals.setdefault((w, row.get("Counter_Name")), []).append(float(row["Counter_Value"]))
+                rows += list(csv.DictReader(fh))
         shutil.rmtree(outdir, ignore_errors=True)
-        for (w, c), v in vals.items():
-            res[w][c] = float(np.median(v))
-    return res, ("per launch, median over the child's launches; FETCH_SIZE doubled (gfx950 reports half the "
-                 "bytes of a wide coalesced read, MI355X_MICROARCH.md) + WRITE_SIZE, both KiB; valu_busy = "
-                 "4 x SQ_ACTIVE_INST_VALU / (%d SIMDs x GRBM_GUI_ACTIVE / %d XCDs) (rocprof's VALUBusy formula, "
-                 "SQ_ACTIVE_INST_* in quad-cycles); configs 2/3 measured at <= 10M keys" % (SIMDS, XCDS))
+        for w, cs in parse_pmc_rows(rows, grids).items():
+            for c, v in cs.items():
+                res[w][c] = float(np.median(v))
+    return res, ("per launch, median over the child's launches of each workload's kernel at its own grid size; "
+                 "configs 2/3 at <= 10M keys. traffic = FETCH_SIZE x the factor that turns the FETCH_SIZE of a "
+                 "same-run ceiling pattern of known bytes into those bytes (fetch_factor, fetch_factor_from) + "
+                 "WRITE_SIZE, KiB -> B. valu_busy = 4 x SQ_ACTIVE_INST_VALU / (%d SIMDs x GRBM_GUI_ACTIVE / %d XCDs) "
+                 "(rocprof's VALUBusy formula); valu_busy_range = it divided by the same formula's reading on the "
+                 "two VALU-saturating launches (half- and full-rate instructions): the kernel's true VALU "
+                 "occupancy lies between. wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES" % (SIMDS, XCDS))
 
 
-def pmc_fields(c, algorithmic_bytes):
+def valu_formula(c):
+    if c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
+        return 4.0 * c["SQ_ACTIVE_INST_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS)
+    return None
+
+
+def pmc_calibration(pmc):
+    """Factors from the ceiling patterns of known bytes: FETCH_SIZE (KiB) ->
+    bytes read, WRITE_SIZE -> bytes written; the VALUBusy formula's reading on
+    the saturating launches."""
+    cal = {}
+    for w, per_lane in CEIL_READ_PER_LANE.items():
+        c = (pmc or {}).get(w)
+        if c and c.get("FETCH_SIZE"):
+            cal[w] = {"fetch_factor": round(c["_lanes"] * per_lane / (c["FETCH_SIZE"] * 1024.0), 4)}
+            if c.get("WRITE_SIZE"):
+                cal[w]["write_factor"] = round(c["_lanes"] * 16 / (c["WRITE_SIZE"] * 1024.0), 4)
+    for w in ("ceil_valu_add", "ceil_valu_mul"):
+        c = (pmc or {}).get(w)
+        if c and valu_formula(c):
+            cal[w] = {"valu_formula_reading": round(valu_formula(c), 4)}
+    return cal
+
+
+def pmc_fields(c, algorithmic_bytes, fetch_factor=2.0, valu_sat=None):
+    """Derived counters of one workload (c: per-launch medians, KiB for the sizes)."""
     out = {}
     if c.get("FETCH_SIZE") is not None and c.get("WRITE_SIZE") is not None:
-        t = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        t = (fetch_factor * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
         out["traffic"] = t
         out["traffic_over_algorithmic"] = round(t / algorithmic_bytes, 4) if algorithmic_bytes else None
-    if c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
-        out["valu_busy"] = round(4.0 * c["SQ_ACTIVE_INST_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS), 4)
+    v = valu_formula(c)
+    if v is not None:
+        out["valu_busy"] = round(v, 4)
+        if valu_sat:
+            out["valu_busy_range"] = [round(v / max(valu_sat), 4), round(v / min(valu_sat), 4)]
+    if c.get("SQ_WAIT_ANY") and c.get("SQ_WAVE_CYCLES"):
+        out["wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
     return out
 
 
-def limiter(achieved_gbs, valu_busy):
-    """Which resource is closer to its ceiling: the HBM (against the measured
-    copy ceiling) or the VALU."""
-    h = achieved_gbs / HBM_COPY_GBS
-    if valu_busy is None:
+def limiter(frac_of_ceiling, valu_hi):
+    """Which resource is closer to its ceiling: the HBM (the line's rate over
+    the measured ceiling of its shape) or the VALU (upper estimate)."""
+    if frac_of_ceiling is None:
+        return "unknown (ceiling not measured in this run)"
+    if valu_hi is None:
         return "hbm (valu not measured)"
-    return "hbm" if h >= valu_busy else "valu"
+    return "hbm" if frac_of_ceiling >= valu_hi else "valu"
 
 
 # ---------------------------------------------------------------------------
@@ -746,17 +980,136 @@ def summarize(w, walls, devs, steps, keys_total):
     vals = [keys_total / t for t in walls]
     i_med = int(np.argsort(vals)[len(vals) // 2])
     per_launch = devs[i_med]
+    ops = getattr(w, "ops_per_key", 1)
     return {
-        "value": vals[i_med],
-        "value_min": min(vals), "value_max": max(vals), "repeats": len(vals),
+        "value": vals[i_med] * ops,
+        "value_min": min(vals) * ops, "value_max": max(vals) * ops, "repeats": len(vals),
         "ms_per_step": 1e3 * walls[i_med] / steps,
         "kernel_us": per_launch * 1e6,
         "achieved_gbs": w.n * w.bytes_per_key / per_launch / 1e9,
         "bytes_per_key": w.bytes_per_key,
+        "lanes": w.n,
         "kernel": w.kernel,
         "desc": w.desc,
         "enqueue_us_per_step": 1e6 * w.enqueue_s / steps,
     }
+
+
+def roofline_of(name, r, results, pmc, cal, args):
+    """roofline object of one line: algorithmic GB/s over the spec peak and
+    over the ceiling of the same shape measured in this run; PMC traffic with
+    a calibrated FETCH_SIZE factor; VALU busy (formula and calibrated range)."""
+    ceil_name = CEILING_OF.get(name)
+    ceil = results.get(ceil_name) if ceil_name else None
+    ro = {"bound": "hbm", "achieved": round(r["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+          "frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+          "bytes_per_key": round(r["bytes_per_key"], 2), "kernel": r["kernel"],
+          "kernel_us": round(r["kernel_us"], 2),
+          "kernel_us_note": "HIP events on the launch stream around the K back-to-back launches / K (inter-kernel "
+                            "gaps included)"}
+    if name.startswith("ceil_valu"):
+        ro["bound"], ro["unit"], ro["peak"] = "valu", "lane-ops/s", None
+        ro["achieved"], ro["frac"] = r["value"], None
+    if ceil is not None:
+        ro["copy_ceiling"] = {"workload": ceil_name, "gbs": round(ceil["achieved_gbs"], 1),
+                              "kernel_us": round(ceil["kernel_us"], 2)}
+        ro["frac_of_copy_ceiling"] = round(r["achieved_gbs"] / ceil["achieved_gbs"], 4)
+    elif ceil_name:
+        ro["frac_of_copy_ceiling"] = None
+        ro["copy_ceiling"] = "%s not measured in this run" % ceil_name
+    key = {"fixed16_hot": "fixed16", "shard1b": "fixed16", "ceil_copy_hot": "ceil_copy",
+           "ceil_copy_1b": "ceil_copy"}.get(name, name)
+    c = (pmc or {}).get(key)
+    valu_sat = [cal[w]["valu_formula_reading"] for w in ("ceil_valu_add", "ceil_valu_mul") if w in cal]
+    if c and len(c) > 1:
+        lanes = c["_lanes"]
+        fsrc = FETCH_CAL_OF.get(key, key if key in CEIL_READ_PER_LANE else None)
+        ff = cal.get(fsrc, {}).get("fetch_factor") if fsrc else None
+        f = pmc_fields(c, lanes * r["bytes_per_key"], ff if ff else 2.0, valu_sat if len(valu_sat) == 2 else None)
+        ro["fetch_factor"] = ff if ff else 2.0
+        ro["fetch_factor_from"] = fsrc if ff else "MI355X_MICROARCH.md (x2, 16-B streams; no calibration this run)"
+        ro["fetch_size_raw"] = c.get("FETCH_SIZE", 0) * 1024.0
+        ro["write_size"] = c.get("WRITE_SIZE", 0) * 1024.0
+        if lanes == r["lanes"]:
+            ro["traffic"] = f.get("traffic")
+        else:
+            ro["traffic_at_pmc_size"] = f.get("traffic")
+            ro["pmc_lanes"] = lanes
+        for k in ("traffic_over_algorithmic", "valu_busy", "valu_busy_range", "wait_frac"):
+            if k in f:
+                ro[k] = f[k]
+    vr = ro.get("valu_busy_range")
+    ro["limiter"] = limiter(ro.get("frac_of_copy_ceiling"), vr[1] if vr else ro.get("valu_busy"))
+    return ro
+
+
+def build_line(args, world, n_gpus, shared, results, verified, per_rank, units, pmc, pmc_note, cpu, host_inc,
+               shards):
+    """rank 0's JSON line from the reduced results (pure: no GPU, tested on the CPU)."""
+    head_name = "fixed16" if "fixed16" in results else next(iter(results))
+    head = results[head_name]
+    cal = pmc_calibration(pmc)
+    roof = roofline_of(head_name, head, results, pmc, cal, args)
+    roof["algorithmic_bytes_per_launch"] = int(head["bytes_per_key"] * args.keys16) if head_name == "fixed16" \
+        else None
+    roof["traffic_note"] = pmc_note
+    secondary = {}
+    for name, r in results.items():
+        if name == head_name:
+            continue
+        secondary[name] = {"value": r["value"], "value_min": r["value_min"], "value_max": r["value_max"],
+                           "unit": units.get(name, "keys/s"), "ms_per_step": round(r["ms_per_step"], 4),
+                           "desc": r["desc"], "roofline": roofline_of(name, r, results, pmc, cal, args),
+                           "verified": verified.get(name)}
+        if name == "shard1b":
+            secondary[name]["scaling"] = "strong"
+            secondary[name]["shards"] = shards
+    all_ok = all(v["ok"] is True for v in verified.values()) if verified else None
+    line = {
+        "metric": METRIC,
+        "value": head["value"],
+        "unit": "keys/s",
+        "n_gpus": n_gpus,
+        "ranks": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "repeats": args.repeats,
+        "value_min": head["value_min"],
+        "value_max": head["value_max"],
+        "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: random key bytes generated on device (torch Philox), resident in HBM before timing",
+        "config": {"workload": "BASELINE configs[1]: %d fixed 16-B keys per GPU per step, MurmurHash3_x64_128 "
+                               "seed 12345 -> 16-B SHF_HASH (shf_make_hash batch), rotating over %d distinct "
+                               "batches" % (args.keys16, max(1, args.rotate)),
+                   "keys_per_gpu": args.keys16, "key_len": 16,
+                   "parallelism": "dp%d (independent key shards, no collective)" % n_gpus},
+        "roofline": roof,
+        "verified": all_ok,
+        "verification": verified,
+        "cpu_baseline": cpu,
+        "host_inclusive": host_inc,
+        "secondary": secondary,
+    }
+    if cal:
+        line["pmc_calibration"] = cal
+    if world > 1:
+        line["per_rank"] = per_rank
+        spread = {}
+        for name in results:
+            ks = [pr["kernel_us"].get(name) for pr in per_rank if pr["kernel_us"].get(name)]
+            if len(ks) == len(per_rank):
+                spread[name] = round(max(ks) / min(ks), 4)
+        line["slowest_over_fastest_rank"] = spread
+        line["barrier_backend"] = args.dist_backend
+    if shared:
+        line["rehearsal"] = True
+        line["rehearsal_note"] = "%d ranks shared %d GPU(s) (--allow-shared-gpu): throughput is not a " \
+                                 "multi-GPU measurement" % (world, n_gpus)
+    return line
 
 
 def run_rank(args):
@@ -772,29 +1125,27 @@ def run_rank(args):
     if world > 1:
         import torch.distributed as tdist
 
-        backend = args.dist_backend
-        if backend == "auto":
-            backend = "gloo" if shared else "nccl"
-        if backend == "nccl":  # RCCL: barriers + max-reduces, no data path
+        if args.dist_backend == "nccl":  # RCCL: barriers + max-reduces only, no data path
             if shared:
                 raise SystemExit("bench.py: RCCL cannot run two ranks on one GPU; use --dist-backend gloo")
             tdist.init_process_group("nccl", device_id=dev)
             dist_dev = dev
-        else:
+        else:  # gloo on CPU tensors: no data crosses GPUs, so no RCCL init is needed
             tdist.init_process_group("gloo")
         dist = tdist
     hb.check_device()
     n_gpus = min(world, torch.cuda.device_count()) if shared else world
 
     wl = make_workloads(args, dev, rank, world)
-    results = {}
-    verified = {}
+    results, verified, mine = {}, {}, {"kernel_us": {}, "verified": {}}
     for w in wl:
-        walls, devs = time_workload(w, args.steps, args.warmup, args.repeats, dist, dist_dev, args.warmup_min_s)
+        walls, devs, devs_local = time_workload(w, args.steps, args.warmup, args.repeats, dist, dist_dev,
+                                                args.warmup_min_s)
         keys_total = (w.job_keys or w.n * world) * args.steps
         r = results[w.name] = summarize(w, walls, devs, args.steps, keys_total)
-        log(args, "[bench] %s: %.3f Gkeys/s (min %.3f, max %.3f), %.1f us/launch, %.0f GB/s, enqueue %.1f us/step"
-            % (w.name, r["value"] / 1e9, r["value_min"] / 1e9, r["value_max"] / 1e9, r["kernel_us"],
+        mine["kernel_us"][w.name] = round(float(np.median(devs_local)) * 1e6, 2)
+        log(args, "[bench] %s: %.4g %s (min %.4g, max %.4g), %.1f us/launch, %.0f GB/s, enqueue %.1f us/step"
+            % (w.name, r["value"], getattr(w, "unit", "keys/s"), r["value_min"], r["value_max"], r["kernel_us"],
                r["achieved_gbs"], r["enqueue_us_per_step"]))
         if not args.no_verify and w.verify is not None:
             try:
@@ -802,6 +1153,7 @@ def run_rank(args):
             except Exception as e:  # noqa: BLE001
                 ok, checked = None, 0
                 log(args, "[bench] %s: verify unavailable: %s" % (w.name, e))
+            mine["verified"][w.name] = ok
             if dist:
                 t = torch.tensor([1 if ok else (0 if ok is False else -1)], dtype=torch.int64, device=dist_dev)
                 dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -811,102 +1163,27 @@ def run_rank(args):
                 raise SystemExit("bench.py: %s outputs differ from the oracle" % w.name)
     shards = None
     sw = next((w for w in wl if w.name == "shard1b"), None)
-    if sw is not None and dist:
-        t = torch.zeros(2 * world, dtype=torch.int64, device=dist_dev)
-        t[2 * rank], t[2 * rank + 1] = sw.shard[0], sw.shard[1]
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        shards = [[int(t[2 * r]), int(t[2 * r + 1])] for r in range(world)]
-    elif sw is not None:
+    if sw is not None:
         shards = [list(sw.shard)]
+    per_rank = None
+    if dist:
+        mine.update(rank=rank, device=dev_idx, device_name=torch.cuda.get_device_name(dev),
+                    shard=list(sw.shard) if sw is not None else None)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        per_rank = sorted(gathered, key=lambda x: x["rank"])
+        if sw is not None:
+            shards = [pr["shard"] for pr in per_rank]
 
     if rank == 0:
         pmc, pmc_note = None, "not collected"
         if world == 1 and args.traffic == "auto":
             pmc, pmc_note = collect_pmc(args, list(results))
-        head_name = "fixed16" if "fixed16" in results else next(iter(results))
-        head = results[head_name]
-
-        def roofline(name, r):
-            ro = {"bound": "hbm", "achieved": round(r["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
-                  "frac_of_copy_ceiling": round(r["achieved_gbs"] / HBM_COPY_GBS, 4),
-                  "bytes_per_key": round(r["bytes_per_key"], 2), "kernel": r["kernel"],
-                  "kernel_us": round(r["kernel_us"], 2)}
-            c = (pmc or {}).get(name if name not in ("fixed16_hot", "shard1b") else "fixed16")
-            if c:
-                # keys per launch in the PMC child (configs 2/3 run there at <= 10M keys)
-                pk = {"fixed256": min(args.keys256, 10_000_000), "var": min(args.keysvar, 10_000_000),
-                      "tabpart": args.tab_jobs}.get(name, args.keys16)
-                f = pmc_fields(c, pk * r["bytes_per_key"])
-                if name in FETCH_UNCALIBRATED:
-                    ro["fetch_size_raw"] = c.get("FETCH_SIZE", 0) * 1024.0
-                    ro["write_size"] = c.get("WRITE_SIZE", 0) * 1024.0
-                    ro["fetch_x2_uncalibrated"] = FETCH_UNCALIBRATED[name]
-                if name in ("fixed16", "fixed16_hot", "probe16", "tabpart"):
-                    ro["traffic"] = f.get("traffic")
-                else:
-                    ro["traffic_at_pmc_size"] = f.get("traffic")
-                ro["traffic_over_algorithmic"] = f.get("traffic_over_algorithmic")
-                ro["valu_busy"] = f.get("valu_busy")
-            ro["limiter"] = limiter(r["achieved_gbs"], ro.get("valu_busy"))
-            return ro
-
-        roof = roofline(head_name, head)
-        roof["algorithmic_bytes_per_launch"] = int(head["bytes_per_key"] * args.keys16) if head_name == "fixed16" \
-            else None
-        roof["traffic_note"] = pmc_note
-        secondary = {}
-        wmap = {w.name: w for w in wl}
-        for name, r in results.items():
-            if name == head_name:
-                continue
-            secondary[name] = {"value": r["value"], "value_min": r["value_min"], "value_max": r["value_max"],
-                               "unit": getattr(wmap[name], "unit", "keys/s"), "ms_per_step": round(r["ms_per_step"], 4),
-                               "desc": r["desc"],
-                               "roofline": roofline(name, r), "verified": verified.get(name)}
-            if name == "shard1b":
-                secondary[name]["scaling"] = "strong"
-                secondary[name]["shards"] = shards
-        cpu = None
-        if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args)
-        host_inc = None
-        if world == 1 and not args.no_host_inclusive:
-            host_inc = time_host_inclusive(args, dev)
-        all_ok = all(v["ok"] is True for v in verified.values()) if verified else None
-        line = {
-            "metric": METRIC,
-            "value": head["value"],
-            "unit": "keys/s",
-            "n_gpus": n_gpus,
-            "ranks": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "repeats": args.repeats,
-            "value_min": head["value_min"],
-            "value_max": head["value_max"],
-            "ms_per_step": head["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic: random key bytes generated on device (torch Philox), resident in HBM before timing",
-            "config": {"workload": "BASELINE configs[1]: %d fixed 16-B keys per GPU per step, MurmurHash3_x64_128 "
-                                   "seed 12345 -> 16-B SHF_HASH (shf_make_hash batch), rotating over %d distinct "
-                                   "batches" % (args.keys16, max(1, args.rotate)),
-                       "keys_per_gpu": args.keys16, "key_len": 16,
-                       "parallelism": "dp%d (independent key shards, no collective)" % n_gpus},
-            "roofline": roof,
-            "verified": all_ok,
-            "verification": verified,
-            "cpu_baseline": cpu,
-            "host_inclusive": host_inc,
-            "secondary": secondary,
-        }
-        if shared:
-            line["rehearsal"] = True
-            line["rehearsal_note"] = "%d ranks shared %d GPU(s) (--allow-shared-gpu): throughput is not a " \
-                                     "multi-GPU measurement" % (world, n_gpus)
+        cpu = cpu_baseline(args) if world == 1 and not args.no_cpu else None
+        host_inc = time_host_inclusive(args, dev) if world == 1 and not args.no_host_inclusive else None
+        units = {w.name: getattr(w, "unit", "keys/s") for w in wl}
+        line = build_line(args, world, n_gpus, shared, results, verified, per_rank, units, pmc, pmc_note, cpu,
+                          host_inc, shards)
         os.write(args.json_fd, (json.dumps(line) + "\n").encode())
     if dist:
         dist.barrier()

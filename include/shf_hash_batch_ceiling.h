@@ -26,6 +26,10 @@ extern "C" {
                                    row pre-probe, + 16-B store: 148 B; every idx[i] < src_bytes / 128 (caller's duty) */
 #define SHF_HB_CEIL_STREAM16U 3 /* 16-B load at src + 16 i + shift (byte-unaligned: shift = 7 for an aligned src)
                                    + 16-B store: 32 B; src_bytes >= 16 n + 16 */
+#define SHF_HB_CEIL_VALU_ADD 4  /* no loads: 8 independent v_add_u32 chains per lane, src_bytes rounds (the loop
+                                   count; d_src any non-NULL value, not read), one 16-B store: a VALU-saturating
+                                   launch of full-rate instructions (8 x src_bytes per lane) */
+#define SHF_HB_CEIL_VALU_MUL 5  /* the same with v_mul_lo_u32 (half rate on gfx950) */
 
 /* Enqueue one launch on hip_stream. Device pointers; dst 16-B aligned, n x 16 B. */
 SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,

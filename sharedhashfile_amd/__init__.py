@@ -99,7 +99,16 @@ _SIGS = {
     "shf_hash_batch_last_hip_error": [],
     "shf_hash_batch_strerror": [_INT],
     "shf_hash_batch_version": [],
+    "shf_hb_ceiling_async": [_INT, _VP, _U64, _VP, _VP, _U64, _VP],  # include/shf_hash_batch_ceiling.h
 }
+
+# include/shf_hash_batch_ceiling.h: the on-box HBM ceilings bench.py measures
+CEIL_COPY = 0
+CEIL_READ16 = 1
+CEIL_GATHER128 = 2
+CEIL_STREAM16U = 3
+CEIL_VALU_ADD = 4
+CEIL_VALU_MUL = 5
 
 
 def load(path=None):
@@ -116,7 +125,11 @@ def load(path=None):
         pass
     lib = ctypes.CDLL(p)
     for name, args in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if path is None:  # the in-tree build must export everything
+                raise RuntimeError("%s does not export %s: rebuild it" % (p, name))
+            continue  # an older variant loaded side by side for an A/B (tools/ab.py)
         fn.argtypes = args
         fn.restype = ctypes.c_char_p if name in ("shf_hash_batch_strerror", "shf_hash_batch_version") else ctypes.c_int
     if path is None:

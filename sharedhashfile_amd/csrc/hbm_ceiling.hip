@@ -18,6 +18,12 @@
 //                    byte-unaligned, as the tab copy's record gathers load), one
 //                    16-B store to dst[i]. 32 B per lane, each source line read
 //                    once (a calibration of FETCH_SIZE for unaligned loads).
+//   k_ceil_valu<MUL> no memory traffic but one 16-B store per lane: 8
+//                    independent chains of v_add_u32 (MUL = 0) or v_mul_lo_u32
+//                    (MUL = 1) per lane, `iters` rounds -- a VALU-saturating
+//                    launch, to read what rocprof's VALUBusy formula reports for
+//                    a SIMD that is busy every cycle with full-rate or with
+//                    half-rate instructions (tools/probe_valu.hip's rates).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -81,6 +87,27 @@ __global__ __launch_bounds__(kBlock) void k_ceil_stream16u(const uint8_t* __rest
   dst[i] = *reinterpret_cast<g_u32x4_a1*>(reinterpret_cast<uintptr_t>(src) + 16u * i + shift);
 }
 
+#define SHFHB_OP8(INS)                                                                                   \
+  asm volatile(INS " %0, %0, %8\n\t" INS " %1, %1, %8\n\t" INS " %2, %2, %8\n\t" INS " %3, %3, %8\n\t" INS \
+               " %4, %4, %8\n\t" INS " %5, %5, %8\n\t" INS " %6, %6, %8\n\t" INS " %7, %7, %8"               \
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)          \
+               : "v"(k))
+
+template <int MUL>
+__global__ __launch_bounds__(kBlock) void k_ceil_valu(uint32_t seed, u32x4* __restrict__ dst, uint64_t n,
+                                                      uint32_t iters) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  uint32_t a0 = (uint32_t)i ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+           a7 = a0 + 7;
+  const uint32_t k = seed | 1u;
+  for (uint32_t r = 0; r < iters; ++r) {
+    if constexpr (MUL) SHFHB_OP8("v_mul_lo_u32");
+    else SHFHB_OP8("v_add_u32");
+  }
+  if (i < n) dst[i] = u32x4{a0 ^ a1, a2 ^ a3, a4 ^ a5, a6 ^ a7};
+}
+#undef SHFHB_OP8
+
 }  // namespace
 }  // namespace shfhb
 
@@ -112,6 +139,17 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
       const uint32_t shift = (uint32_t)(((uintptr_t)d_src) & 15u) ? 0u : 7u;  // aligned base: read 7 bytes in
       if (src_bytes < 16u * n + 16u) return SHF_HB_ERR_ARG;
       hipLaunchKernelGGL(k_ceil_stream16u, grid, block, 0, st, (const uint8_t*)d_src, (u32x4*)d_dst, n, shift);
+      break;
+    }
+    case SHF_HB_CEIL_VALU_ADD:
+    case SHF_HB_CEIL_VALU_MUL: {
+      // d_src is not read; src_bytes is the loop count per lane
+      if (src_bytes == 0 || src_bytes > 0xffffffffull) return SHF_HB_ERR_ARG;
+      const uint32_t iters = (uint32_t)src_bytes, seed = (uint32_t)(uintptr_t)d_src;
+      if (kind == SHF_HB_CEIL_VALU_ADD)
+        hipLaunchKernelGGL(k_ceil_valu<0>, grid, block, 0, st, seed, (u32x4*)d_dst, n, iters);
+      else
+        hipLaunchKernelGGL(k_ceil_valu<1>, grid, block, 0, st, seed, (u32x4*)d_dst, n, iters);
       break;
     }
     default:

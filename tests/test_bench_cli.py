@@ -73,8 +73,90 @@ def test_summarize_reports_median_and_spread():
 
 def test_pmc_fields_and_limiter():
     f = bench.pmc_fields({"FETCH_SIZE": 100.0, "WRITE_SIZE": 50.0, "SQ_ACTIVE_INST_VALU": 1024.0,
-                          "GRBM_GUI_ACTIVE": 8.0}, 250 * 1024.0)
+                          "GRBM_GUI_ACTIVE": 8.0, "SQ_WAIT_ANY": 30.0, "SQ_WAVE_CYCLES": 100.0}, 250 * 1024.0,
+                         fetch_factor=2.0, valu_sat=[2.0, 4.0])
     assert f["traffic"] == 250 * 1024.0 and f["traffic_over_algorithmic"] == 1.0
-    assert f["valu_busy"] == 4.0
-    assert bench.limiter(6000.0, 0.5) == "hbm"
-    assert bench.limiter(3000.0, 0.9) == "valu"
+    assert f["valu_busy"] == 4.0 and f["valu_busy_range"] == [1.0, 2.0]
+    assert f["wait_frac"] == 0.3
+    assert bench.limiter(0.95, 0.5) == "hbm"
+    assert bench.limiter(0.5, 0.9) == "valu"
+    assert bench.limiter(None, 0.9).startswith("unknown")
+
+
+def test_rank_envs_for_eight_gpus():
+    envs = bench.rank_envs(8, 29500, base={"PATH": "/bin"})
+    assert [e["RANK"] for e in envs] == [str(r) for r in range(8)]
+    assert [e["LOCAL_RANK"] for e in envs] == [str(r) for r in range(8)]
+    assert all(e["WORLD_SIZE"] == e["LOCAL_WORLD_SIZE"] == "8" and e["MASTER_ADDR"] == "127.0.0.1"
+               and e["MASTER_PORT"] == "29500" and e["PATH"] == "/bin" for e in envs)
+    # every rank its own GPU on an 8-GPU node
+    assert [bench.plan_device(r, 8, 8, False) for r in range(8)] == [(r, False) for r in range(8)]
+
+
+def test_grid_threads_match_the_launchers():
+    assert bench.grid_threads("fixed16", 10_000_000) == 10_000_128
+    assert bench.grid_threads("fixed256", 100) == 128
+    assert bench.grid_threads("var", 100_000_000) == 781_250 * 128  # 1 562 500 tiles, two per workgroup
+    assert bench.grid_threads("var", 65) == 128
+    assert bench.grid_threads("tabpart", 1024) == 1024 * 512
+    assert bench.grid_threads("ceil_read16", 64) == 256
+
+
+def test_parse_pmc_rows_keys_on_kernel_and_grid():
+    rows = [{"Kernel_Name": "void shfhb::k_fixed16<0>(...)", "Grid_Size": "256", "Counter_Name": "FETCH_SIZE",
+             "Counter_Value": "10"},
+            {"Kernel_Name": "void shfhb::k_fixed16<0>(...)", "Grid_Size": "512", "Counter_Name": "FETCH_SIZE",
+             "Counter_Value": "99"},
+            {"Kernel_Name": "shfhb::(anonymous namespace)::k_ceil_copy(...)", "Grid_Size": "256",
+             "Counter_Name": "FETCH_SIZE", "Counter_Value": "5"}]
+    v = bench.parse_pmc_rows(rows, {"fixed16": 256, "ceil_copy": 256})
+    assert v == {"fixed16": {"FETCH_SIZE": [10.0]}, "ceil_copy": {"FETCH_SIZE": [5.0]}}
+
+
+def _fake_result(name, gbs, us=50.0, lanes=10_000_000, bpk=32.0):
+    return {"value": 1e11, "value_min": 0.9e11, "value_max": 1.1e11, "repeats": 3, "ms_per_step": 0.05,
+            "kernel_us": us, "achieved_gbs": gbs, "bytes_per_key": bpk, "lanes": lanes, "kernel": "k", "desc": name,
+            "enqueue_us_per_step": 5.0}
+
+
+def _args(**kw):
+    a = bench.parse(["--no-cpu", "--traffic", "off"])
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_roofline_divides_by_the_ceiling_measured_in_the_run():
+    results = {"fixed16": _fake_result("fixed16", 6000.0), "ceil_copy": _fake_result("ceil_copy", 6400.0),
+               "var": _fake_result("var", 5200.0, lanes=100_000_000, bpk=284.0)}
+    pmc = {"fixed16": {"_lanes": 10_000_000, "FETCH_SIZE": 160e6 / 2 / 1024, "WRITE_SIZE": 160e6 / 1024},
+           "ceil_copy": {"_lanes": 10_000_000, "FETCH_SIZE": 160e6 / 2 / 1024, "WRITE_SIZE": 160e6 / 1024}}
+    cal = bench.pmc_calibration(pmc)
+    assert cal["ceil_copy"] == {"fetch_factor": 2.0, "write_factor": 1.0}
+    ro = bench.roofline_of("fixed16", results["fixed16"], results, pmc, cal, _args())
+    assert ro["frac_of_copy_ceiling"] == round(6000.0 / 6400.0, 4)
+    assert ro["copy_ceiling"]["workload"] == "ceil_copy"
+    assert ro["frac"] == 0.75 and ro["traffic"] == 320e6 and ro["traffic_over_algorithmic"] == 1.0
+    assert ro["fetch_factor_from"] == "ceil_copy"
+    # no read-mostly ceiling in this run: no fraction (never a constant)
+    rv = bench.roofline_of("var", results["var"], results, pmc, cal, _args())
+    assert rv["frac_of_copy_ceiling"] is None and "not measured" in rv["copy_ceiling"]
+
+
+def test_line_for_eight_ranks_carries_per_rank_fields():
+    world = 8
+    results = {"fixed16": _fake_result("fixed16", 6000.0), "ceil_copy": _fake_result("ceil_copy", 6300.0)}
+    per_rank = [{"rank": r, "device": r, "device_name": "AMD Instinct MI355X", "shard": None,
+                 "kernel_us": {"fixed16": 50.0 + r, "ceil_copy": 48.0}, "verified": {"fixed16": True}}
+                for r in range(world)]
+    verified = {"fixed16": {"ok": True, "samples_per_rank": 20002}}
+    line = bench.build_line(_args(), world, world, False, results, verified, per_rank,
+                            {"fixed16": "keys/s", "ceil_copy": "lanes/s"}, None, "not collected", None, None, None)
+    assert line["n_gpus"] == 8 and line["ranks"] == 8 and "rehearsal" not in line
+    assert [p["device"] for p in line["per_rank"]] == list(range(8))
+    assert line["slowest_over_fastest_rank"]["fixed16"] == round(57.0 / 50.0, 4)
+    assert line["slowest_over_fastest_rank"]["ceil_copy"] == 1.0
+    assert line["barrier_backend"] == "gloo"
+    assert line["verified"] is True and line["secondary"]["ceil_copy"]["unit"] == "lanes/s"
+    json_line = bench.json.dumps(line)
+    assert "all_visible_cpus_extrapolated" not in json_line and "HBM_COPY" not in json_line

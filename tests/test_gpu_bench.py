@@ -5,7 +5,8 @@
 * the same run as a labelled rehearsal (--allow-shared-gpu) spawns 2 rank
   processes that each hash their own contiguous shard of the 1B keys through
   the product library: shards [0, 5e8) and [5e8, 1e9), disjoint and complete,
-  outputs checked against the oracle on every rank, `n_gpus` = distinct GPUs.
+  outputs checked against the oracle on every rank, `n_gpus` = distinct GPUs,
+  and the line carries each rank's device, kernel times and verdicts.
 """
 import json
 import os
@@ -59,3 +60,13 @@ def test_two_rank_rehearsal_shards_configs4():
     assert line["verified"] is True
     # value = all ranks' keys / max-over-ranks time
     assert line["value"] == pytest.approx(2 * 1_000_000 * 5 / (line["ms_per_step"] * 5 / 1e3), rel=1e-6)
+    # per-rank evidence: device, own kernel times and verdicts, the shard each took
+    pr = line["per_rank"]
+    assert [p["rank"] for p in pr] == [0, 1]
+    assert [p["device"] for p in pr] == [r % max(1, ndev) for r in range(2)]
+    assert all(p["kernel_us"]["fixed16"] > 0 and p["kernel_us"]["shard1b"] > 0 for p in pr)
+    assert all(p["verified"]["fixed16"] is True and p["verified"]["shard1b"] is True for p in pr)
+    assert [p["shard"] for p in pr] == sh["shards"]
+    assert set(line["slowest_over_fastest_rank"]) == {"fixed16", "shard1b"}
+    assert all(v >= 1.0 for v in line["slowest_over_fastest_rank"].values())
+    assert line["barrier_backend"] == "gloo"

@@ -46,7 +46,7 @@ def fixed_kernels(key_len, aligned=True):
     return ks
 
 
-VAR_KERNELS = [0, 3, 4, 5]  # AUTO, GENERIC, SPAN, ROUND
+VAR_KERNELS = [0, 3, 4, 5, 6]  # AUTO, GENERIC, SPAN, ROUND, SPAN_PP
 
 
 # ---------------------------------------------------------------------------
@@ -317,6 +317,28 @@ def test_var_long_keys(hb, dev, oracle):
     for k in VAR_KERNELS:
         got = u64(hb.hash_var(d_u8(data, dev), d_off(off, dev), kernel=k))
         assert np.array_equal(got, want), k
+
+
+@pytest.mark.parametrize("lo,hi", [(8, 2048), (400, 1200)])
+def test_var_long_keys_without_byte_count(hb, dev, oracle, lo, hi):
+    """Keys whose 64-key spans overflow the 20-KiB window, hashed without a
+    byte count (AUTO -> k_span_pp) and through SHF_HB_KERNEL_SPAN_PP: the
+    overflowing tiles are streamed through the window in rounds in their
+    wave's turn (they used to be hashed per lane from HBM)."""
+    rng = np.random.default_rng(lo + hi)
+    n = 64 * 700 + 13
+    lens = rng.integers(lo, hi + 1, size=n)
+    lens[64 * 5 + 3] = 9000  # a key past the round path's 8 KiB: that tile per lane from HBM
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]) + 5, dtype=np.uint8)
+    want = oracle.hash_var(data, off)
+    d_data, d_o = d_u8(data, dev), d_off(off, dev)
+    for k in (0, 6):
+        assert np.array_equal(u64(hb.hash_var(d_data, d_o, kernel=k)), want), k
+    # shifted start: every key unaligned
+    d_o3 = d_off(off + np.uint64(3), dev)
+    assert np.array_equal(u64(hb.hash_var(d_data, d_o3, kernel=6)), oracle.hash_var(data[3:], off))
 
 
 @pytest.mark.parametrize("base", [(1 << 31) + 12345, (1 << 32) + 12345, (3 << 31) + 7])

@@ -140,6 +140,40 @@ def test_malformed_jobs_fail_without_fault(hb, dev):
     assert np.array_equal(keep, want[:size])
 
 
+def test_refs_repeating_one_large_record_fail(hb, dev):
+    """A corrupt image whose 8192 refs all name one 2-MiB record: each ref is
+    inside the image, their lengths sum to 16 GiB. The u32 size scans would
+    wrap to exactly 0 per segment (2048 x 2 MiB = 2^32); the exact u64 total
+    rejects the job -- status ERR_ARG, no fault, nothing past cap."""
+    lib = hb.load()
+    data_off = 24 + 512 * 16 * 8
+    rec = 1 << 21  # SHF_DATA_TYPE + u32 key length + key + u32 value length (0) = 2 MiB
+    kl = rec - 9
+    img = np.zeros(data_off + rec, dtype=np.uint8)
+    img[data_off] = 0x3E
+    img[data_off + 1:data_off + 5] = np.frombuffer(np.uint32(kl).tobytes(), np.uint8)
+    hdr = img[:24].view(np.uint32)
+    hdr[:] = [img.size, img.size, 2 * 8192, 0, 1, rec]  # tab_data_free != 0: the length-word path
+    rows = img[24:data_off].view(np.uint32).reshape(-1, 2)
+    rows[:, 0] = 5 | (123 << 11)
+    rows[:, 1] = data_off
+    size = img.size
+    src = torch.from_numpy(img).to(dev)
+    dst = torch.zeros(size + 4096, dtype=torch.uint8, device=dev)
+    jobs = (hb.TabJob * 1)()
+    j = jobs[0]
+    j.src, j.src_len, j.keep, j.move, j.cap, j.map, j.tab_new = 0, size, 0, 0, size, 0, 0xFFFF
+    j.keep_type, j.move_type, j.status = 0x3E, 0x3E, 99
+    d_jobs = torch.from_numpy(np.frombuffer(bytes(jobs), dtype=np.uint8).copy()).to(dev)
+    prm = hb.TabParams(0, 0, 0, 1)
+    rc = lib.shf_tab_copy_batch(src.data_ptr(), size, dst.data_ptr(), dst.numel(), d_jobs.data_ptr(), 1, None, 0,
+                                ctypes.byref(prm), hb.MEM_DEVICE)
+    assert rc == hb.ERR_ARG
+    done = (hb.TabJob * 1).from_buffer_copy(d_jobs.cpu().numpy().tobytes())
+    assert done[0].status == hb.ERR_ARG
+    assert not dst[size:].any().item()  # nothing written past cap
+
+
 def test_host_memory_entry_point(hb, dev):
     lib = hb.load()
     cap = fixture_caps()[1]

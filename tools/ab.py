@@ -2,11 +2,14 @@
 """Interleaved A/B timing of library build variants in ONE process
 (cdna_hip_programming.md s5.4 rule 24).
 
-    python tools/ab.py --variant base= --variant nodist=-DSHFHB_CHAIN_DISTRIBUTED=0 \
-        --workload fixed256 --n 20000000 --rounds 8
+    python tools/ab.py --variant base= --variant exp=@tools/_ab/lib_exp.so \
+        --workload var --n 25000000 --rounds 8
 
-Each variant is the same sources built with extra -D flags into its own .so
-(loaded side by side through ctypes); every round times every variant once.
+`name=` is the in-tree build; `name=@path.so` a library built beforehand on
+the CPU host from an experimental copy of the sources (the library itself has
+no compile-time alternatives: tests/test_abi.py); `name=-Dflags` builds the
+in-tree sources with extra flags. The variants are loaded side by side through
+ctypes; every round times every variant once.
 """
 import argparse
 import ctypes

@@ -1,17 +1,18 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSV output: mean counter value per kernel.
+"""Summarise rocprofv3 --pmc CSV output: median counter value per (kernel, grid).
 
     python tools/pmc_summary.py <dir containing *counter_collection.csv> [kernel-substring ...]
 """
 import collections
 import csv
+import statistics
 import glob
 import os
 import sys
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     return name.replace("void ", "").replace("shfhb::", "")
 
 
@@ -25,12 +26,12 @@ def main():
                 raw = row["Kernel_Name"]
                 if want and not any(w in raw for w in want):
                     continue
-                k = short(raw)
+                k = "%s  grid %s" % (short(raw), row.get("Grid_Size", "?"))
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, cs in sorted(acc.items()):
         print(k)
         for c, v in sorted(cs.items()):
-            print("   %-28s %16.1f  (n=%d)" % (c, sum(v) / len(v), len(v)))
+            print("   %-28s %16.1f  (median of n=%d)" % (c, statistics.median(v), len(v)))
 
 
 if __name__ == "__main__":
