@@ -72,23 +72,31 @@ BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for 
 # are also matched on the launch's grid size, Workload.grid)
 KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
                "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>",
-               "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy", "ceil_copy_hot": "k_ceil_copy",
-               "ceil_copy_1b": "k_ceil_copy", "ceil_read16": "k_ceil_read16", "ceil_gather128": "k_ceil_gather128",
+               "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy(", "ceil_copy_hot": "k_ceil_copy(",
+               "ceil_copy_1b": "k_ceil_copy(", "ceil_read16": "k_ceil_read16", "ceil_gather128": "k_ceil_gather128",
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
-               "ceil_valu_mul": "k_ceil_valu<1>"}
+               "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copy4": "k_ceil_copy4(", "ceil_copy4_hot": "k_ceil_copy4(",
+               "ceil_copy4_1b": "k_ceil_copy4(", "ceil_probe_rows": "k_ceil_gather128"}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart"]
-CEIL_WORKLOADS = ["ceil_copy", "ceil_copy_hot", "ceil_copy_1b", "ceil_read16", "ceil_gather128", "ceil_stream16u",
-                  "ceil_valu_add", "ceil_valu_mul"]
-# the ceiling each hashing line is reported against: the copy of the same shape on the same buffers
-CEILING_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy_hot", "shard1b": "ceil_copy_1b",
-              "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128", "tabpart": "ceil_copy"}
+CEIL_WORKLOADS = ["ceil_copy", "ceil_copy4", "ceil_copy_hot", "ceil_copy4_hot", "ceil_copy_1b", "ceil_copy4_1b",
+                  "ceil_read16", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
+                  "ceil_valu_mul"]
+# the ceiling each hashing line is reported against: the best copy of the same bytes on the same buffers
+# (one lane per 16 B as k_fixed16 moves them, or four), measured in this run right after the line
+CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copy4"], "fixed16_hot": ["ceil_copy_hot", "ceil_copy4_hot"],
+              "shard1b": ["ceil_copy_1b", "ceil_copy4_1b"], "fixed256": ["ceil_read16"], "var": ["ceil_read16"],
+              "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copy4"]}
+# timing order: each ceiling right after the line it bounds (same buffers, same thermal state)
+ORDER = ["fixed16", "ceil_copy", "ceil_copy4", "fixed16_hot", "ceil_copy_hot", "ceil_copy4_hot", "shard1b",
+         "ceil_copy_1b", "ceil_copy4_1b", "fixed256", "ceil_read16", "var", "probe16", "ceil_probe_rows",
+         "ceil_gather128", "tabpart", "ceil_stream16u", "ceil_valu_add", "ceil_valu_mul"]
 # the pattern whose known byte count calibrates each line's FETCH_SIZE
 FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
                 "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
                 "tabpart": "ceil_stream16u"}
 # bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
-CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copy_hot": 16, "ceil_copy_1b": 16, "ceil_read16": 256,
-                      "ceil_gather128": 132, "ceil_stream16u": 16}
+CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copy4": 16, "ceil_read16": 256, "ceil_gather128": 132,
+                      "ceil_stream16u": 16}
 VALU_ITERS = 2048          # rounds of 8 chained VALU ops per lane in the VALU-saturating launches
 VALU_LANES = 256 * 32 * 64  # 32 waves per CU on 256 CUs
 
@@ -289,6 +297,8 @@ def _up(x, m):
 def grid_threads(name, n):
     """Work-items of one launch of workload `name` over n keys / lanes / jobs:
     rocprofv3's Grid_Size of that launch (the PMC rows are matched on it)."""
+    if name.startswith("ceil_copy4"):
+        return _up(n, 1024) // 4        # 256-thread blocks of 4 x 16 B per lane
     if name in ("fixed16", "fixed16_hot", "shard1b", "probe16") or name.startswith("ceil_"):
         return _up(n, 256)              # 256-thread blocks, one key / lane per thread
     if name == "fixed256":
@@ -359,7 +369,7 @@ def make_workloads(args, dev, rank, world=1):
                                "256 MiB Infinity Cache)" % n,
                                lambda p=pairs[:1]: verify_fixed(p, 16, VERIFY_SAMPLES, 12),
                                grid_threads("fixed16_hot", n)))
-    if "shard1b" in only or "ceil_copy_1b" in only:
+    if "shard1b" in only or "ceil_copy_1b" in only or "ceil_copy4_1b" in only:
         # configs[4]: 1B 16-B keys split evenly over the job's GPUs (strong scaling:
         # 1B / world keys on this rank, contiguous index range, no collective).
         from sharedhashfile_amd.shard import shard_range
@@ -418,7 +428,12 @@ def make_workloads(args, dev, rank, world=1):
         tab_slot, rows, n_slots, placed = synthetic_index(h, tabs_per_win=args.probe_tabs)
         index = hb.RowIndex(n_slots, tab_slot, rows)
         host_index = (tab_slot.cpu().numpy().view(np.uint32), rows.cpu().numpy(), n_slots)
-        del h, tab_slot, rows
+        # each key's row (slot * 512 + row) in key order: the probe's own row sequence, for its ceiling
+        h1 = h[:, 0]
+        T = args.probe_tabs
+        rid = (((h1 & 0xFF) * T + ((h1 >> 16) & 0x7FF) % T) * 512 + ((h1 >> 32) & 0x1FF)).to(torch.int32)
+        bufs["probe_rows"] = (rows, rid, n)
+        del h, tab_slot, h1
         out = torch.empty((n, 4), dtype=torch.int32, device=dev)
 
         def verify_probe(keys=keys, out=out, hx=host_index):
@@ -445,7 +460,7 @@ def make_workloads(args, dev, rank, world=1):
         wl.append(tab_workload(args, dev, seed_base))
     wl += ceiling_workloads(args, dev, only, bufs, fixed16_pairs)
     torch.cuda.synchronize()
-    return wl
+    return sorted(wl, key=lambda w: ORDER.index(w.name) if w.name in ORDER else len(ORDER))
 
 
 def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
@@ -472,12 +487,39 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
                                [ceil_launcher(hb, hb.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
                                "k_ceil_copy", "the same copy over fixed16_hot's single batch",
                                grid=grid_threads("ceil_copy_hot", n)))
-    if "ceil_copy_1b" in only:
+    if "ceil_copy4" in only or "ceil_copy4_hot" in only:
+        pairs = fixed16_pairs()
+        n = args.keys16
+        if "ceil_copy4" in only:
+            wl.append(Workload("ceil_copy4", n, 32,
+                               [ceil_launcher(hb, hb.CEIL_COPY4, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
+                                for k, o in pairs], "k_ceil_copy4",
+                               "16-B units, 4 per lane, over fixed16's %d rotating batches" % len(pairs),
+                               grid=grid_threads("ceil_copy4", n)))
+        if "ceil_copy4_hot" in only:
+            k, o = pairs[0]
+            wl.append(Workload("ceil_copy4_hot", n, 32,
+                               [ceil_launcher(hb, hb.CEIL_COPY4, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
+                               "k_ceil_copy4", "the same over fixed16_hot's single batch",
+                               grid=grid_threads("ceil_copy4_hot", n)))
+    for name, kind, kern in (("ceil_copy_1b", hb.CEIL_COPY, "k_ceil_copy"), ("ceil_copy4_1b", hb.CEIL_COPY4,
+                                                                                "k_ceil_copy4")):
+        if name not in only:
+            continue
         keys, out, n = bufs["shard1b"]
-        wl.append(Workload("ceil_copy_1b", n, 32,
-                           [ceil_launcher(hb, hb.CEIL_COPY, keys.data_ptr(), 16 * n, None, out.data_ptr(), n, dev)],
-                           "k_ceil_copy", "the same copy over shard1b's %d keys + hashes" % n,
-                           grid=grid_threads("ceil_copy_1b", n)))
+        wl.append(Workload(name, n, 32,
+                           [ceil_launcher(hb, kind, keys.data_ptr(), 16 * n, None, out.data_ptr(), n, dev)],
+                           kern, "the same copy over shard1b's %d keys + hashes" % n, grid=grid_threads(name, n)))
+    if "ceil_probe_rows" in only and "probe_rows" in bufs:
+        rows, rid, n = bufs["probe_rows"]
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        wl.append(Workload("ceil_probe_rows", n, 148,
+                           [ceil_launcher(hb, hb.CEIL_GATHER128, rows.data_ptr(), rows.numel(), rid.data_ptr(),
+                                          out.data_ptr(), n, dev)], "k_ceil_gather128",
+                           "probe16's own row reads without the hash: each key's 128-B row (its slot and row, in key "
+                           "order) fetched 8 lanes per row + 4-B index + 16-B store per lane, %d lanes" % n,
+                           grid=grid_threads("ceil_probe_rows", n)))
+        wl[-1].keep = (rows, rid, out)
     if "ceil_read16" in only:
         n = read16_lanes(args, only)
         if "fixed256" in bufs:
@@ -846,7 +888,8 @@ def cpu_baseline(args):
 PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"],
               ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                "GRBM_GUI_ACTIVE"]]
-PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b")  # same kernels and grids as measured ones
+PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b", "ceil_copy4_hot", "ceil_copy4_1b",
+            "ceil_probe_rows")  # same kernels and grids as measured ones
 
 
 def pmc_child_sizes(args, want):
@@ -855,7 +898,8 @@ def pmc_child_sizes(args, want):
     k256, kvar = min(args.keys256, 10_000_000), min(args.keysvar, 10_000_000)
     child = argparse.Namespace(keys256=k256, keys16=args.keys16)
     sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
-             "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_read16": read16_lanes(child, set(want)),
+             "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_copy4": args.keys16,
+             "ceil_read16": read16_lanes(child, set(want)),
              "ceil_gather128": args.keys16, "ceil_stream16u": 2 * args.keys16, "ceil_valu_add": VALU_LANES,
              "ceil_valu_mul": VALU_LANES}
     return {w: sizes[w] for w in want if w in sizes}, k256, kvar
@@ -999,7 +1043,8 @@ def roofline_of(name, r, results, pmc, cal, args):
     """roofline object of one line: algorithmic GB/s over the spec peak and
     over the ceiling of the same shape measured in this run; PMC traffic with
     a calibrated FETCH_SIZE factor; VALU busy (formula and calibrated range)."""
-    ceil_name = CEILING_OF.get(name)
+    cands = [c for c in CEILING_OF.get(name, []) if c in results]
+    ceil_name = max(cands, key=lambda c: results[c]["achieved_gbs"]) if cands else None
     ceil = results.get(ceil_name) if ceil_name else None
     ro = {"bound": "hbm", "achieved": round(r["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
           "frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
@@ -1014,11 +1059,11 @@ def roofline_of(name, r, results, pmc, cal, args):
         ro["copy_ceiling"] = {"workload": ceil_name, "gbs": round(ceil["achieved_gbs"], 1),
                               "kernel_us": round(ceil["kernel_us"], 2)}
         ro["frac_of_copy_ceiling"] = round(r["achieved_gbs"] / ceil["achieved_gbs"], 4)
-    elif ceil_name:
+    elif name in CEILING_OF:
         ro["frac_of_copy_ceiling"] = None
-        ro["copy_ceiling"] = "%s not measured in this run" % ceil_name
+        ro["copy_ceiling"] = "%s not measured in this run" % " / ".join(CEILING_OF[name])
     key = {"fixed16_hot": "fixed16", "shard1b": "fixed16", "ceil_copy_hot": "ceil_copy",
-           "ceil_copy_1b": "ceil_copy"}.get(name, name)
+           "ceil_copy_1b": "ceil_copy", "ceil_copy4_hot": "ceil_copy4", "ceil_copy4_1b": "ceil_copy4"}.get(name, name)
     c = (pmc or {}).get(key)
     valu_sat = [cal[w]["valu_formula_reading"] for w in ("ceil_valu_add", "ceil_valu_mul") if w in cal]
     if c and len(c) > 1:

@@ -30,6 +30,7 @@ extern "C" {
                                    count; d_src any non-NULL value, not read), one 16-B store: a VALU-saturating
                                    launch of full-rate instructions (8 x src_bytes per lane) */
 #define SHF_HB_CEIL_VALU_MUL 5  /* the same with v_mul_lo_u32 (half rate on gfx950) */
+#define SHF_HB_CEIL_COPY4 6     /* SHF_HB_CEIL_COPY's bytes, 4 x 16 B per lane (1024 units per 256-thread block) */
 
 /* Enqueue one launch on hip_stream. Device pointers; dst 16-B aligned, n x 16 B. */
 SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,

@@ -109,6 +109,7 @@ CEIL_GATHER128 = 2
 CEIL_STREAM16U = 3
 CEIL_VALU_ADD = 4
 CEIL_VALU_MUL = 5
+CEIL_COPY4 = 6
 
 
 def load(path=None):

@@ -6,6 +6,9 @@
 //   k_ceil_copy      lane i: one 16-B nontemporal load of src[i], one 16-B store
 //                    to dst[i]; 256-thread blocks, one lane per 16 B -- k_fixed16's
 //                    shape (configs[1]) without the hash. 32 B per lane.
+//   k_ceil_copy4     the same bytes, 4 x 16 B per lane (a block copies 1024
+//                    consecutive 16-B units, lane l units l, l + 256, ...): more
+//                    loads in flight per wave than k_fixed16's shape allows.
 //   k_ceil_read16    lane i: 16 x 16-B nontemporal loads (its wave reads one
 //                    contiguous 16-KiB span, 1 KiB per instruction, the way k_tiled
 //                    and k_span stage a tile), their XOR stored as 16 B. 272 B per
@@ -44,6 +47,18 @@ __global__ __launch_bounds__(kBlock) void k_ceil_copy(const u32x4* __restrict__ 
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   dst[i] = __builtin_nontemporal_load(&src[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ceil_copy4(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       uint64_t n) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * (4 * kBlock) + threadIdx.x;
+  u32x4 v[4];
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q)
+    if (i0 + q * kBlock < n) v[q] = __builtin_nontemporal_load(&src[i0 + q * kBlock]);
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q)
+    if (i0 + q * kBlock < n) dst[i0 + q * kBlock] = v[q];
 }
 
 __global__ __launch_bounds__(kBlock) void k_ceil_read16(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
@@ -124,6 +139,11 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
     case SHF_HB_CEIL_COPY:
       if (!al16 || src_bytes < 16u * n) return SHF_HB_ERR_ARG;
       hipLaunchKernelGGL(k_ceil_copy, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
+      break;
+    case SHF_HB_CEIL_COPY4:
+      if (!al16 || src_bytes < 16u * n) return SHF_HB_ERR_ARG;
+      hipLaunchKernelGGL(k_ceil_copy4, dim3((unsigned)((n + 4 * kBlock - 1) / (4 * kBlock))), block, 0, st,
+                         (const u32x4*)d_src, (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_READ16:
       if (!al16 || n % 64u || src_bytes < 256u * n) return SHF_HB_ERR_ARG;
