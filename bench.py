@@ -75,27 +75,28 @@ KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1
                "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy(", "ceil_copy_hot": "k_ceil_copy(",
                "ceil_copy_1b": "k_ceil_copy(", "ceil_read16": "k_ceil_read16", "ceil_gather128": "k_ceil_gather128",
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
-               "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copy4": "k_ceil_copy4(", "ceil_copy4_hot": "k_ceil_copy4(",
-               "ceil_copy4_1b": "k_ceil_copy4(", "ceil_probe_rows": "k_ceil_gather128"}
+               "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
+               "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128"}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart"]
-CEIL_WORKLOADS = ["ceil_copy", "ceil_copy4", "ceil_copy_hot", "ceil_copy4_hot", "ceil_copy_1b", "ceil_copy4_1b",
+CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
                   "ceil_read16", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
                   "ceil_valu_mul"]
 # the ceiling each hashing line is reported against: the best copy of the same bytes on the same buffers
-# (one lane per 16 B as k_fixed16 moves them, or four), measured in this run right after the line
-CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copy4"], "fixed16_hot": ["ceil_copy_hot", "ceil_copy4_hot"],
-              "shard1b": ["ceil_copy_1b", "ceil_copy4_1b"], "fixed256": ["ceil_read16"], "var": ["ceil_read16"],
-              "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copy4"]}
+# (one lane per 16 B as k_fixed16 moves them, plain or nontemporal stores), measured in this run right after
+# the line
+CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copynt"], "fixed16_hot": ["ceil_copy_hot", "ceil_copynt_hot"],
+              "shard1b": ["ceil_copy_1b", "ceil_copynt_1b"], "fixed256": ["ceil_read16"], "var": ["ceil_read16"],
+              "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copynt"]}
 # timing order: each ceiling right after the line it bounds (same buffers, same thermal state)
-ORDER = ["fixed16", "ceil_copy", "ceil_copy4", "fixed16_hot", "ceil_copy_hot", "ceil_copy4_hot", "shard1b",
-         "ceil_copy_1b", "ceil_copy4_1b", "fixed256", "ceil_read16", "var", "probe16", "ceil_probe_rows",
+ORDER = ["fixed16", "ceil_copy", "ceil_copynt", "fixed16_hot", "ceil_copy_hot", "ceil_copynt_hot", "shard1b",
+         "ceil_copy_1b", "ceil_copynt_1b", "fixed256", "ceil_read16", "var", "probe16", "ceil_probe_rows",
          "ceil_gather128", "tabpart", "ceil_stream16u", "ceil_valu_add", "ceil_valu_mul"]
 # the pattern whose known byte count calibrates each line's FETCH_SIZE
 FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
                 "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
                 "tabpart": "ceil_stream16u"}
 # bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
-CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copy4": 16, "ceil_read16": 256, "ceil_gather128": 132,
+CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copynt": 16, "ceil_read16": 256, "ceil_gather128": 132,
                       "ceil_stream16u": 16}
 VALU_ITERS = 2048          # rounds of 8 chained VALU ops per lane in the VALU-saturating launches
 VALU_LANES = 256 * 32 * 64  # 32 waves per CU on 256 CUs
@@ -297,8 +298,6 @@ def _up(x, m):
 def grid_threads(name, n):
     """Work-items of one launch of workload `name` over n keys / lanes / jobs:
     rocprofv3's Grid_Size of that launch (the PMC rows are matched on it)."""
-    if name.startswith("ceil_copy4"):
-        return _up(n, 1024) // 4        # 256-thread blocks of 4 x 16 B per lane
     if name in ("fixed16", "fixed16_hot", "shard1b", "probe16") or name.startswith("ceil_"):
         return _up(n, 256)              # 256-thread blocks, one key / lane per thread
     if name == "fixed256":
@@ -369,7 +368,7 @@ def make_workloads(args, dev, rank, world=1):
                                "256 MiB Infinity Cache)" % n,
                                lambda p=pairs[:1]: verify_fixed(p, 16, VERIFY_SAMPLES, 12),
                                grid_threads("fixed16_hot", n)))
-    if "shard1b" in only or "ceil_copy_1b" in only or "ceil_copy4_1b" in only:
+    if "shard1b" in only or "ceil_copy_1b" in only or "ceil_copynt_1b" in only:
         # configs[4]: 1B 16-B keys split evenly over the job's GPUs (strong scaling:
         # 1B / world keys on this rank, contiguous index range, no collective).
         from sharedhashfile_amd.shard import shard_range
@@ -487,23 +486,23 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
                                [ceil_launcher(hb, hb.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
                                "k_ceil_copy", "the same copy over fixed16_hot's single batch",
                                grid=grid_threads("ceil_copy_hot", n)))
-    if "ceil_copy4" in only or "ceil_copy4_hot" in only:
+    if "ceil_copynt" in only or "ceil_copynt_hot" in only:
         pairs = fixed16_pairs()
         n = args.keys16
-        if "ceil_copy4" in only:
-            wl.append(Workload("ceil_copy4", n, 32,
-                               [ceil_launcher(hb, hb.CEIL_COPY4, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
-                                for k, o in pairs], "k_ceil_copy4",
-                               "16-B units, 4 per lane, over fixed16's %d rotating batches" % len(pairs),
-                               grid=grid_threads("ceil_copy4", n)))
-        if "ceil_copy4_hot" in only:
+        if "ceil_copynt" in only:
+            wl.append(Workload("ceil_copynt", n, 32,
+                               [ceil_launcher(hb, hb.CEIL_COPY_NT, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
+                                for k, o in pairs], "k_ceil_copyv<1>",
+                               "the same copy with nontemporal stores (the fastest of tools/copy_sweep.py's variants) "
+                               "over fixed16's %d rotating batches" % len(pairs), grid=grid_threads("ceil_copynt", n)))
+        if "ceil_copynt_hot" in only:
             k, o = pairs[0]
-            wl.append(Workload("ceil_copy4_hot", n, 32,
-                               [ceil_launcher(hb, hb.CEIL_COPY4, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
-                               "k_ceil_copy4", "the same over fixed16_hot's single batch",
-                               grid=grid_threads("ceil_copy4_hot", n)))
-    for name, kind, kern in (("ceil_copy_1b", hb.CEIL_COPY, "k_ceil_copy"), ("ceil_copy4_1b", hb.CEIL_COPY4,
-                                                                                "k_ceil_copy4")):
+            wl.append(Workload("ceil_copynt_hot", n, 32,
+                               [ceil_launcher(hb, hb.CEIL_COPY_NT, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
+                               "k_ceil_copyv<1>", "the same over fixed16_hot's single batch",
+                               grid=grid_threads("ceil_copynt_hot", n)))
+    for name, kind, kern in (("ceil_copy_1b", hb.CEIL_COPY, "k_ceil_copy"), ("ceil_copynt_1b", hb.CEIL_COPY_NT,
+                                                                                "k_ceil_copyv<1>")):
         if name not in only:
             continue
         keys, out, n = bufs["shard1b"]
@@ -888,7 +887,7 @@ def cpu_baseline(args):
 PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"],
               ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                "GRBM_GUI_ACTIVE"]]
-PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b", "ceil_copy4_hot", "ceil_copy4_1b",
+PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b", "ceil_copynt_hot", "ceil_copynt_1b",
             "ceil_probe_rows")  # same kernels and grids as measured ones
 
 
@@ -898,7 +897,7 @@ def pmc_child_sizes(args, want):
     k256, kvar = min(args.keys256, 10_000_000), min(args.keysvar, 10_000_000)
     child = argparse.Namespace(keys256=k256, keys16=args.keys16)
     sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
-             "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_copy4": args.keys16,
+             "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
              "ceil_read16": read16_lanes(child, set(want)),
              "ceil_gather128": args.keys16, "ceil_stream16u": 2 * args.keys16, "ceil_valu_add": VALU_LANES,
              "ceil_valu_mul": VALU_LANES}
@@ -1063,7 +1062,7 @@ def roofline_of(name, r, results, pmc, cal, args):
         ro["frac_of_copy_ceiling"] = None
         ro["copy_ceiling"] = "%s not measured in this run" % " / ".join(CEILING_OF[name])
     key = {"fixed16_hot": "fixed16", "shard1b": "fixed16", "ceil_copy_hot": "ceil_copy",
-           "ceil_copy_1b": "ceil_copy", "ceil_copy4_hot": "ceil_copy4", "ceil_copy4_1b": "ceil_copy4"}.get(name, name)
+           "ceil_copy_1b": "ceil_copy", "ceil_copynt_hot": "ceil_copynt", "ceil_copynt_1b": "ceil_copynt"}.get(name, name)
     c = (pmc or {}).get(key)
     valu_sat = [cal[w]["valu_formula_reading"] for w in ("ceil_valu_add", "ceil_valu_mul") if w in cal]
     if c and len(c) > 1:

@@ -31,6 +31,11 @@ extern "C" {
                                    launch of full-rate instructions (8 x src_bytes per lane) */
 #define SHF_HB_CEIL_VALU_MUL 5  /* the same with v_mul_lo_u32 (half rate on gfx950) */
 #define SHF_HB_CEIL_COPY4 6     /* SHF_HB_CEIL_COPY's bytes, 4 x 16 B per lane (1024 units per 256-thread block) */
+/* the same bytes as SHF_HB_CEIL_COPY, other instruction choices (the sweep that picks the ceiling) */
+#define SHF_HB_CEIL_COPY_PLAIN 7 /* plain loads */
+#define SHF_HB_CEIL_COPY_NT 8    /* nontemporal loads and stores */
+#define SHF_HB_CEIL_COPY_SLEEP 9 /* nontemporal loads, a short s_sleep before the store */
+#define SHF_HB_CEIL_COPY2 10     /* two 16-B units per lane */
 
 /* Enqueue one launch on hip_stream. Device pointers; dst 16-B aligned, n x 16 B. */
 SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,

@@ -110,6 +110,10 @@ CEIL_STREAM16U = 3
 CEIL_VALU_ADD = 4
 CEIL_VALU_MUL = 5
 CEIL_COPY4 = 6
+CEIL_COPY_PLAIN = 7
+CEIL_COPY_NT = 8
+CEIL_COPY_SLEEP = 9
+CEIL_COPY2 = 10
 
 
 def load(path=None):

@@ -49,6 +49,34 @@ __global__ __launch_bounds__(kBlock) void k_ceil_copy(const u32x4* __restrict__ 
   dst[i] = __builtin_nontemporal_load(&src[i]);
 }
 
+// Variants of the one-lane-per-16-B copy (tools/copy_sweep.py picks the best for bench.py):
+// V = 0 plain loads, 1 nt loads + nt stores, 2 nt loads + s_sleep between load and store (the hash's
+// delay: reads and writes of a wave further apart), 3 two units per lane (block-strided)
+template <int V>
+__global__ __launch_bounds__(kBlock) void k_ceil_copyv(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       uint64_t n) {
+  if constexpr (V == 3) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * (2 * kBlock) + threadIdx.x;
+    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+    if (i0 < n) a = __builtin_nontemporal_load(&src[i0]);
+    if (i0 + kBlock < n) b = __builtin_nontemporal_load(&src[i0 + kBlock]);
+    if (i0 < n) dst[i0] = a;
+    if (i0 + kBlock < n) dst[i0 + kBlock] = b;
+    return;
+  }
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  if constexpr (V == 0) {
+    dst[i] = src[i];
+  } else if constexpr (V == 1) {
+    __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+  } else {
+    const u32x4 v = __builtin_nontemporal_load(&src[i]);
+    __builtin_amdgcn_s_sleep(3);
+    dst[i] = v;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_ceil_copy4(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                        uint64_t n) {
   const uint64_t i0 = (uint64_t)blockIdx.x * (4 * kBlock) + threadIdx.x;
@@ -145,6 +173,20 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
       hipLaunchKernelGGL(k_ceil_copy4, dim3((unsigned)((n + 4 * kBlock - 1) / (4 * kBlock))), block, 0, st,
                          (const u32x4*)d_src, (u32x4*)d_dst, n);
       break;
+    case SHF_HB_CEIL_COPY_PLAIN:
+    case SHF_HB_CEIL_COPY_NT:
+    case SHF_HB_CEIL_COPY_SLEEP:
+    case SHF_HB_CEIL_COPY2: {
+      if (!al16 || src_bytes < 16u * n) return SHF_HB_ERR_ARG;
+      const dim3 g2((unsigned)((n + 2 * kBlock - 1) / (2 * kBlock)));
+      const u32x4* s4 = (const u32x4*)d_src;
+      u32x4* d4 = (u32x4*)d_dst;
+      if (kind == SHF_HB_CEIL_COPY_PLAIN) hipLaunchKernelGGL(k_ceil_copyv<0>, grid, block, 0, st, s4, d4, n);
+      else if (kind == SHF_HB_CEIL_COPY_NT) hipLaunchKernelGGL(k_ceil_copyv<1>, grid, block, 0, st, s4, d4, n);
+      else if (kind == SHF_HB_CEIL_COPY_SLEEP) hipLaunchKernelGGL(k_ceil_copyv<2>, grid, block, 0, st, s4, d4, n);
+      else hipLaunchKernelGGL(k_ceil_copyv<3>, g2, block, 0, st, s4, d4, n);
+      break;
+    }
     case SHF_HB_CEIL_READ16:
       if (!al16 || n % 64u || src_bytes < 256u * n) return SHF_HB_ERR_ARG;
       hipLaunchKernelGGL(k_ceil_read16, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);

@@ -100,7 +100,7 @@ def test_grid_threads_match_the_launchers():
     assert bench.grid_threads("var", 65) == 128
     assert bench.grid_threads("tabpart", 1024) == 1024 * 512
     assert bench.grid_threads("ceil_read16", 64) == 256
-    assert bench.grid_threads("ceil_copy4", 10_000_000) == 2_500_096
+    assert bench.grid_threads("ceil_copynt", 10_000_000) == 10_000_128
 
 
 def test_parse_pmc_rows_keys_on_kernel_and_grid():
@@ -110,11 +110,11 @@ def test_parse_pmc_rows_keys_on_kernel_and_grid():
              "Counter_Value": "99"},
             {"Kernel_Name": "shfhb::(anonymous namespace)::k_ceil_copy(...)", "Grid_Size": "256",
              "Counter_Name": "FETCH_SIZE", "Counter_Value": "5"},
-            {"Kernel_Name": "shfhb::(anonymous namespace)::k_ceil_copy4(...)", "Grid_Size": "256",
+            {"Kernel_Name": "void shfhb::(anonymous namespace)::k_ceil_copyv<1>(...)", "Grid_Size": "256",
              "Counter_Name": "FETCH_SIZE", "Counter_Value": "7"}]
-    v = bench.parse_pmc_rows(rows, {"fixed16": 256, "ceil_copy": 256, "ceil_copy4": 256})
+    v = bench.parse_pmc_rows(rows, {"fixed16": 256, "ceil_copy": 256, "ceil_copynt": 256})
     assert v == {"fixed16": {"FETCH_SIZE": [10.0]}, "ceil_copy": {"FETCH_SIZE": [5.0]},
-                 "ceil_copy4": {"FETCH_SIZE": [7.0]}}
+                 "ceil_copynt": {"FETCH_SIZE": [7.0]}}
 
 
 def _fake_result(name, gbs, us=50.0, lanes=10_000_000, bpk=32.0):
@@ -132,7 +132,7 @@ def _args(**kw):
 
 def test_roofline_divides_by_the_ceiling_measured_in_the_run():
     results = {"fixed16": _fake_result("fixed16", 6000.0), "ceil_copy": _fake_result("ceil_copy", 6400.0),
-               "ceil_copy4": _fake_result("ceil_copy4", 6300.0),
+               "ceil_copynt": _fake_result("ceil_copynt", 6300.0),
                "var": _fake_result("var", 5200.0, lanes=100_000_000, bpk=284.0)}
     pmc = {"fixed16": {"_lanes": 10_000_000, "FETCH_SIZE": 160e6 / 2 / 1024, "WRITE_SIZE": 160e6 / 1024},
            "ceil_copy": {"_lanes": 10_000_000, "FETCH_SIZE": 160e6 / 2 / 1024, "WRITE_SIZE": 160e6 / 1024}}
