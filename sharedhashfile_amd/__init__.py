@@ -114,6 +114,7 @@ CEIL_COPY_PLAIN = 7
 CEIL_COPY_NT = 8
 CEIL_COPY_SLEEP = 9
 CEIL_COPY2 = 10
+CEIL_READ16_NT = 11
 
 
 def load(path=None):

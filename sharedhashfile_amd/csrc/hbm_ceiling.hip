@@ -13,6 +13,7 @@
 //                    contiguous 16-KiB span, 1 KiB per instruction, the way k_tiled
 //                    and k_span stage a tile), their XOR stored as 16 B. 272 B per
 //                    lane: configs[2]'s 256 + 16 B per key (configs[3]: 284).
+//                    Plain or nontemporal store (the hashing kernels store nt).
 //   k_ceil_gather128 lane i: one 128-B row rows[idx[i]] (the row index read as a
 //                    4-B stream), fetched 8 lanes per row exactly as the probe's
 //                    row fetch does (probe_scan_coop), 16 B stored per lane. With
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(kBlock) void k_ceil_copy4(const u32x4* __restrict__
     if (i0 + q * kBlock < n) dst[i0 + q * kBlock] = v[q];
 }
 
+template <bool NT_STORE>
 __global__ __launch_bounds__(kBlock) void k_ceil_read16(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                         uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -102,7 +104,8 @@ __global__ __launch_bounds__(kBlock) void k_ceil_read16(const u32x4* __restrict_
   u32x4 x = v[0];
 #pragma unroll
   for (int q = 1; q < 16; ++q) x ^= v[q];
-  dst[i] = x;
+  if constexpr (NT_STORE) __builtin_nontemporal_store(x, &dst[i]);
+  else dst[i] = x;
 }
 
 __global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __restrict__ rows,
@@ -188,8 +191,12 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
       break;
     }
     case SHF_HB_CEIL_READ16:
+    case SHF_HB_CEIL_READ16_NT:
       if (!al16 || n % 64u || src_bytes < 256u * n) return SHF_HB_ERR_ARG;
-      hipLaunchKernelGGL(k_ceil_read16, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
+      if (kind == SHF_HB_CEIL_READ16)
+        hipLaunchKernelGGL(k_ceil_read16<false>, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
+      else
+        hipLaunchKernelGGL(k_ceil_read16<true>, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_GATHER128:
       // every idx[i] must name a row inside src: checked by the caller's construction (a permutation
