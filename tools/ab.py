@@ -53,6 +53,8 @@ def main():
     p.add_argument("--var-hi", type=int, default=512)
     p.add_argument("--copy-ref", action="store_true", help="also time torch copy_ of the same byte count")
     p.add_argument("--sized", action="store_true", help="var: pass the batch byte count (sized-window API)")
+    p.add_argument("--sort-chunk", type=int, default=0,
+                   help="var: sort the key lengths within chunks of this many keys (what length bucketing buys)")
     p.add_argument("--warmup-s", type=float, default=1.0, help="untimed calls of every variant for this long first")
     p.add_argument("--unchecked", action="append", default=[], help="variant whose results are not compared (ceilings)")
     p.add_argument("--prebuild", default="", help="build every name=-Dflags variant into this dir and exit")
@@ -123,6 +125,10 @@ def main():
         g = torch.Generator(device=dev)
         g.manual_seed(3)
         lens = torch.randint(a.var_lo, a.var_hi + 1, (n,), generator=g, device=dev, dtype=torch.int64)
+        if a.sort_chunk:
+            c = a.sort_chunk
+            m = n // c * c
+            lens[:m] = torch.sort(lens[:m].view(-1, c), dim=1).values.reshape(-1)
         off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         torch.cumsum(lens, 0, out=off[1:])
         data = device_random_bytes(int(off[-1].item()), 2, dev)
