@@ -995,9 +995,10 @@ constexpr uint32_t kBkRegion = 4096;                        // keys per plan reg
 constexpr uint32_t kBkWinPieces = (kSpanAlloc - kSpanPad) / 16;  // 1276 16-B pieces per window
 constexpr uint32_t kBkPmax = 40;                             // longer keys: per lane from HBM
 constexpr uint32_t kBkLong = kBkPmax + 1;                    // their class
-constexpr uint32_t kBkTilesMax =                             // regular tiles hold >= 31 keys, long ones 64
-    (kBkRegion + kBkWinPieces / kBkPmax - 1) / (kBkWinPieces / kBkPmax) + 2;
-constexpr uint32_t kBkWgsPerRegion = (kBkTilesMax + 1) / 2;  // two tiles per workgroup
+constexpr uint32_t kBkTilesMax =  // regular tiles hold >= 31 keys, long ones 64; rounded up to whole workgroups
+    ((kBkRegion + kBkWinPieces / kBkPmax - 1) / (kBkWinPieces / kBkPmax) + 2 + 1) & ~1u;
+constexpr uint32_t kBkWgsPerRegion = kBkTilesMax / 2;  // two tiles per workgroup
+static_assert(kBkTilesMax % 2 == 0 && kBkWgsPerRegion * 2 == kBkTilesMax, "a workgroup's two tiles are its region's");
 constexpr uint32_t kBkPlanThreads = 256;
 static_assert(kBkRegion <= 8192, "tile positions are 13 bits");
 
