@@ -729,18 +729,21 @@ def time_host_inclusive(args, dev):
     res = {"unit": "keys/s", "note": "never `value`: PCIe-bound; sample = %d keys per batch, median of the "
                                      "timed repeats after one untimed call; *_pinned = page-locked caller buffers "
                                      "(16-B keys: the kernel reads and writes them over PCIe, zero copy), "
-                                     "*_pinned_staged = the same through hipMemcpyAsync both ways" % n}
+                                     "*_pinned_staged = the same through hipMemcpyAsync both ways; "
+                                     "fixed16_pageable = pageable buffers whose interior pages the call page-locks "
+                                     "for the kernel (zero copy), *_pageable_staged = through the staged pipeline"
+                                     % n}
 
-    def _staged(fn):  # page-locked buffers through the copy-engine pipeline (zero copy off)
-        old = os.environ.get("SHF_HB_ZERO_COPY_MAX_KEY")
-        os.environ["SHF_HB_ZERO_COPY_MAX_KEY"] = "0"
+    def _staged(fn, var="SHF_HB_ZERO_COPY_MAX_KEY"):  # through the copy-engine pipeline (zero copy off)
+        old = os.environ.get(var)
+        os.environ[var] = "0"
         try:
             return fn()
         finally:
             if old is None:
-                os.environ.pop("SHF_HB_ZERO_COPY_MAX_KEY", None)
+                os.environ.pop(var, None)
             else:
-                os.environ["SHF_HB_ZERO_COPY_MAX_KEY"] = old
+                os.environ[var] = old
     keys = device_random_bytes(n * 16, 77, dev).cpu().numpy()
     g = torch.Generator(device=dev)
     g.manual_seed(78)
@@ -759,6 +762,8 @@ def time_host_inclusive(args, dev):
     cases = [
         ("fixed16_pageable", lambda: lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, SEED, out.ctypes.data,
                                                               hb.MEM_HOST), 5),
+        ("fixed16_pageable_staged", lambda: _staged(lambda: lib.shf_hash_batch_fixed(
+            keys.ctypes.data, 16, n, SEED, out.ctypes.data, hb.MEM_HOST), "SHF_HB_PAGEABLE_ZERO_COPY"), 5),
         ("fixed16_pinned", lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED, po.data_ptr(), hb.MEM_HOST),
          5),
         ("fixed16_pinned_staged", lambda: _staged(lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED,

@@ -490,19 +490,92 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
   return j;
 }
 
+int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in,
+                   bool zero_copy = true);
+HostJob hash_job(shf_hash128* out);
+
+// Page-locks [p, p + bytes) (whole pages) for one call and unlocks it after.
+struct PageLock {
+  void* p = nullptr;
+  void* dev = nullptr;
+  bool lock(void* at, size_t bytes) {
+    if (hipHostRegister(at, bytes, hipHostRegisterMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    p = at;
+    if (hipHostGetDevicePointer(&dev, at, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return true;
+  }
+  ~PageLock() {
+    if (p && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+  }
+};
+
+// Pageable caller buffers, zero copy. The pages that lie wholly inside the
+// caller's key range and inside its hash range are page-locked for this call
+// (hipHostRegister; per call: 10M x 16-B keys 1.75 vs 1.59 G keys/s staged,
+// profiles/r2/host_zero_copy/probe4.txt) and one kernel reads and writes them
+// over PCIe; the few keys at either end whose bytes or record touch a page
+// the range only partly covers go through the staged pipeline. A partial page
+// is never locked, so calls over neighbouring parts of one buffer (the
+// *_multi shards) never lock, or unlock, a page the other one uses.
+// Returns 1 when it does not apply (then nothing was launched).
+constexpr uint64_t kPage = 4096;
+constexpr uint64_t kPageableZeroCopyMin = (uint64_t)1 << 16;  // keys: below this, locking pages costs more
+
+int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                  const HostJob& job) {
+  const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");
+  if ((e && e[0] == '0') || n < kPageableZeroCopyMin) return 1;
+  const uint64_t kb = reinterpret_cast<uintptr_t>(keys), ob = reinterpret_cast<uintptr_t>(job.hash);
+  const uint64_t kp0 = (kb + kPage - 1) & ~(kPage - 1), kp1 = (kb + n * key_len) & ~(kPage - 1);
+  const uint64_t op0 = (ob + kPage - 1) & ~(kPage - 1), op1 = (ob + n * sizeof(shf_hash128)) & ~(kPage - 1);
+  if (kp1 <= kp0 || op1 <= op0) return 1;
+  // keys [lo, hi): every byte in [kp0, kp1) and every record in [op0, op1)
+  const uint64_t lo = std::max((kp0 - kb + key_len - 1) / key_len, (op0 - ob + 15) / 16);
+  const uint64_t hi = std::min((kp1 - kb) / key_len, (op1 - ob) / 16);
+  if (hi <= lo || hi - lo < kPageableZeroCopyMin) return 1;
+  if (kp1 > op0 && op1 > kp0) return 1;  // key and hash pages overlap: leave it to the pipeline
+  PageLock lk, lo_;
+  if (!lk.lock(reinterpret_cast<void*>(kp0), kp1 - kp0) || !lo_.lock(reinterpret_cast<void*>(op0), op1 - op0))
+    return 1;  // e.g. already page-locked by someone else: the staged pipeline instead
+  const uint8_t* dk = static_cast<const uint8_t*>(lk.dev) + (kb + lo * key_len - kp0);
+  shf_hash128* dh = reinterpret_cast<shf_hash128*>(static_cast<uint8_t*>(lo_.dev) + (ob + lo * 16 - op0));
+  HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, out_sink(dh), shfhb::kOutHash, c->st[0],
+                             shfhb::kKernelAuto));
+  // the ends meanwhile, through the staged pipeline (its slots queue behind the launch on st[0])
+  int rc = SHF_HB_OK;
+  if (lo) rc = host_fixed_run(keys, key_len, lo, seed, hash_job(job.hash), false);
+  if (rc == SHF_HB_OK && hi < n)
+    rc = host_fixed_run(keys + hi * key_len, key_len, n - hi, seed, hash_job(job.hash + hi), false);
+  const hipError_t se = hipStreamSynchronize(c->st[0]);  // before the pages are unlocked
+  if (rc) return rc;
+  HB_TRY(se);
+  return SHF_HB_OK;
+}
+
 // Host-memory fixed-length pipeline on the current device.
-int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in) {
+int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in,
+                   bool zero_copy) {
   const HostJob job = with_direct_out(job_in, n);
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  if (job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
+  if (zero_copy && job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
     void* dk = host_range_device_ptr(keys, (size_t)n * key_len);
     void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)) : nullptr;
     if (dh) {
       HB_TRY(shfhb::launch_fixed(dk, key_len, n, seed, out_sink(dh), shfhb::kOutHash, c->st[0], shfhb::kKernelAuto));
       HB_TRY(hipStreamSynchronize(c->st[0]));
       return SHF_HB_OK;
+    }
+    if (!is_host_pinned(keys) && !is_host_pinned(job.hash)) {
+      rc = host_fixed_pageable_zero_copy(c, keys, key_len, n, seed, job);
+      if (rc != 1) return rc;
     }
   }
   if ((uint64_t)key_len > stage_bytes()) return host_fixed_big(c, keys, key_len, n, seed, job);
