@@ -8,6 +8,7 @@
 // There is deliberately no CPU path: without a gfx950 device every call fails loudly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -55,10 +56,24 @@ int map_hip(hipError_t e) {
   }
 }
 
-#define HB_TRY(expr)                       \
-  do {                                     \
-    hipError_t e_ = (expr);                \
-    if (e_ != hipSuccess) return map_hip(e_); \
+// SHF_HB_DEBUG=1 (read once): every failing HIP call is named on stderr.
+bool debug_errors() {
+  static const bool on = [] {
+    const char* e = getenv("SHF_HB_DEBUG");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+#define HB_TRY(expr)                                                                                  \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) {                                                                           \
+      if (debug_errors())                                                                             \
+        fprintf(stderr, "shf_hash_batch: %s:%d: %s -> %d (%s)\n", __FILE__, __LINE__, #expr, (int)e_, \
+                hipGetErrorString(e_));                                                               \
+      return map_hip(e_);                                                                             \
+    }                                                                                                 \
   } while (0)
 
 constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `const int len`
@@ -491,7 +506,7 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
 }
 
 int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in,
-                   bool zero_copy = true);
+                   bool direct = true);
 HostJob hash_job(shf_hash128* out);
 
 // Page-locks [p, p + bytes) (whole pages) for one call and unlocks it after.
@@ -547,7 +562,9 @@ int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_l
   shf_hash128* dh = reinterpret_cast<shf_hash128*>(static_cast<uint8_t*>(lo_.dev) + (ob + lo * 16 - op0));
   HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, out_sink(dh), shfhb::kOutHash, c->st[0],
                              shfhb::kKernelAuto));
-  // the ends meanwhile, through the staged pipeline (its slots queue behind the launch on st[0])
+  // the ends meanwhile, through the staged pipeline (its slots queue behind the launch on st[0]),
+  // copied through the staging as pageable memory: they may begin inside the pages just locked and
+  // run past them, so they must not be taken for page-locked buffers
   int rc = SHF_HB_OK;
   if (lo) rc = host_fixed_run(keys, key_len, lo, seed, hash_job(job.hash), false);
   if (rc == SHF_HB_OK && hi < n)
@@ -558,14 +575,16 @@ int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_l
   return SHF_HB_OK;
 }
 
-// Host-memory fixed-length pipeline on the current device.
+// Host-memory fixed-length pipeline on the current device. direct = false: the
+// caller's buffers are staged as pageable memory whatever they are (no zero
+// copy, no DMA in place, no direct hash stores).
 int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in,
-                   bool zero_copy) {
-  const HostJob job = with_direct_out(job_in, n);
+                   bool direct) {
+  const HostJob job = direct ? with_direct_out(job_in, n) : job_in;
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  if (zero_copy && job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
+  if (direct && job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
     void* dk = host_range_device_ptr(keys, (size_t)n * key_len);
     void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)) : nullptr;
     if (dh) {
@@ -584,8 +603,8 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   const uint64_t chunk = std::min<uint64_t>(per, n);
   if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk, ns))) return rc;
   if (job.probe && (rc = ensure_probe_staging(c))) return rc;
-  const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
-             probe_pinned = is_host_pinned(job.probe);
+  const bool in_pinned = direct && is_host_pinned(keys), hash_pinned = direct && is_host_pinned(job.hash),
+             probe_pinned = direct && is_host_pinned(job.probe);
   Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += chunk, ++idx) {
