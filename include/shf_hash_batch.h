@@ -146,14 +146,11 @@ SHF_HB_API int shf_hash_batch_var_multi(const void *bytes, const uint64_t *offse
 #define SHF_HB_KERNEL_ROUND 5   /* var only: keys streamed 128 B per round through LDS */
 #define SHF_HB_KERNEL_SPAN_PP 6 /* var only: LDS-staged spans, two tiles per window in turn (what AUTO uses for
                                    spans over 10 KiB or an unknown byte count); not for probes */
-#define SHF_HB_KERNEL_BUCKET 7  /* var only: keys sorted by length per region of 4096, tiles of similar lengths
-                                   gathered into LDS (a stream-ordered device scratch of ~2 B per key for the
-                                   call's duration); not for probes */
 
 SHF_HB_API int shf_hash_batch_fixed_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                       shf_hash128 *d_out, int kernel, void *hip_stream);
-/* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_SPAN_PP, SHF_HB_KERNEL_BUCKET,
- * SHF_HB_KERNEL_ROUND or SHF_HB_KERNEL_GENERIC */
+/* kernel: SHF_HB_KERNEL_AUTO, SHF_HB_KERNEL_SPAN, SHF_HB_KERNEL_SPAN_PP, SHF_HB_KERNEL_ROUND or
+ * SHF_HB_KERNEL_GENERIC */
 SHF_HB_API int shf_hash_batch_var_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                     uint32_t seed, shf_hash128 *d_out, int kernel, void *hip_stream);
 SHF_HB_API int shf_hash_batch_var_sized_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,

@@ -36,7 +36,6 @@ KERNEL_GENERIC = 3
 KERNEL_SPAN = 4
 KERNEL_ROUND = 5
 KERNEL_SPAN_PP = 6
-KERNEL_BUCKET = 7
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libshf_hash_batch.so")

@@ -19,8 +19,7 @@ enum KernelChoice {
   kKernelGeneric = 3,
   kKernelSpan = 4,
   kKernelRound = 5,
-  kKernelSpanPP = 6,
-  kKernelBucket = 7
+  kKernelSpanPP = 6
 };
 
 // Where a kernel's per-key result goes (passed by value as a kernel argument).
@@ -40,12 +39,9 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
 // Key i = bytes[offsets[i] - off_base, offsets[i+1] - off_base); offsets on device.
 // key_bytes: offsets[n] - offsets[0] when the caller knows it (sizes the span
 // kernel's LDS window; 0 = unknown). It never changes results.
-// kKernelBucket needs `scratch` of bucket_scratch_bytes(n) device bytes, untouched
-// by anything else until the launch has run on `st` (the caller's duty).
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
                       const Sink& sink, int out_mode, hipStream_t st, int kernel = kKernelAuto,
-                      uint64_t key_bytes = 0, void* scratch = nullptr);
-size_t bucket_scratch_bytes(uint64_t n);
+                      uint64_t key_bytes = 0);
 
 // *taken = atomic exchange of *word with 0 (one thread).
 hipError_t launch_status_take(uint32_t* word, uint32_t* taken, hipStream_t st);

@@ -973,190 +973,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // ---------------------------------------------------------------------------
-// Length-bucketed spans (variable-length keys; SHF_HB_KERNEL_BUCKET). A
-// 64-key tile of consecutive keys holds its LDS window and its wave's VALU for
-// its LONGEST key (31.5 of 32 blocks on U[8,512] B keys, against a mean of
-// 16.25), so k_span_pp issues about twice the block loops the keys need. Here
-// a plan pass sorts each region of kBkRegion consecutive keys by the 16-B
-// pieces they span (a counting sort in LDS) and cuts the sorted list into
-// tiles whose keys all need about as many pieces: K keys of at most P pieces,
-// K = min(64, window / P), so a tile of long keys has fewer lanes but every
-// tile's loop runs to about its keys' own length. The hashing kernel then
-// gathers each tile's keys piece by piece (coalesced per key: consecutive lanes
-// load one key's consecutive 16-B pieces) into the window, slot s of a tile at
-// s * P * 16, and hashes with k_span_pp's two-waves-per-window hand-over.
-// Extra traffic: the plan reads the offsets and writes a 2-B index per key; the
-// hashing kernel reads that index (12 B/key over 284 on config D). Keys over
-// kBkPmax pieces, and tiles with a malformed key, are hashed per lane from HBM.
-// All of one region's workgroups run on one XCD (blocks b and b + 8 share one),
-// so its keys' shared boundary lines and its 64 KiB of results meet in one L2.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kBkRegion = 4096;                        // keys per plan region
-constexpr uint32_t kBkWinPieces = (kSpanAlloc - kSpanPad) / 16;  // 1276 16-B pieces per window
-constexpr uint32_t kBkPmax = 40;                             // longer keys: per lane from HBM
-constexpr uint32_t kBkLong = kBkPmax + 1;                    // their class
-constexpr uint32_t kBkTilesMax =  // regular tiles hold >= 31 keys, long ones 64; rounded up to whole workgroups
-    ((kBkRegion + kBkWinPieces / kBkPmax - 1) / (kBkWinPieces / kBkPmax) + 2 + 1) & ~1u;
-constexpr uint32_t kBkWgsPerRegion = kBkTilesMax / 2;  // two tiles per workgroup
-static_assert(kBkTilesMax % 2 == 0 && kBkWgsPerRegion * 2 == kBkTilesMax, "a workgroup's two tiles are its region's");
-constexpr uint32_t kBkPlanThreads = 256;
-static_assert(kBkRegion <= 8192, "tile positions are 13 bits");
-
-// One tile of a region's sorted list: keys [pos, pos + K) of it, each needing
-// at most P pieces (P = kBkLong: hashed per lane from HBM).
-__device__ __forceinline__ uint32_t bk_desc(uint32_t pos, uint32_t k, uint32_t p) {
-  return pos | (k << 13) | (p << 20);
-}
-
-__global__ __launch_bounds__(kBkPlanThreads) void k_bucket_plan(const uint8_t* __restrict__ bytes,
-                                                                const uint64_t* __restrict__ offsets,
-                                                                uint64_t off_base, uint64_t n,
-                                                                uint16_t* __restrict__ perm,
-                                                                uint32_t* __restrict__ tiles) {
-  __shared__ uint8_t cls[kBkRegion];
-  __shared__ uint16_t sorted[kBkRegion];
-  __shared__ uint32_t hist[kBkLong + 1], start[kBkLong + 1];
-  const uint32_t t = threadIdx.x;
-  const uint64_t k0 = (uint64_t)blockIdx.x * kBkRegion;
-  const uint32_t nk = (uint32_t)min<uint64_t>(kBkRegion, n - k0);
-  if (t <= kBkLong) hist[t] = 0;
-  __syncthreads();
-  const uintptr_t b = reinterpret_cast<uintptr_t>(bytes);
-  for (uint32_t i = t; i < nk; i += kBkPlanThreads) {
-    const uint64_t o0 = offsets[k0 + i], o1 = offsets[k0 + i + 1];
-    uint32_t c = kBkLong;
-    if (!var_key_bad(o0, o1)) {
-      const uint64_t len = o1 - o0;
-      const uint64_t pc = len ? (((b + (o0 - off_base)) & 15u) + len + 15u) >> 4 : 0u;
-      c = pc <= kBkPmax ? (uint32_t)pc : kBkLong;
-    }
-    cls[i] = (uint8_t)c;
-    atomicAdd(&hist[c], 1u);
-  }
-  __syncthreads();
-  if (t == 0) {  // longest regular class first, the long keys last
-    uint32_t at = 0;
-    for (int c = (int)kBkPmax; c >= 0; --c) {
-      start[c] = at;
-      at += hist[c];
-    }
-    start[kBkLong] = at;
-  }
-  __syncthreads();
-  for (uint32_t i = t; i < nk; i += kBkPlanThreads) sorted[atomicAdd(&start[cls[i]], 1u)] = (uint16_t)i;
-  __syncthreads();
-  for (uint32_t i = t; i < nk; i += kBkPlanThreads) perm[k0 + i] = sorted[i];
-  if (t == 0) {  // cut the sorted list: each tile as many keys as its first (longest) key's pieces allow
-    const uint32_t nreg = nk - hist[kBkLong];
-    uint32_t pos = 0, tt = 0;
-    while (pos < nreg) {
-      const uint32_t pf = cls[sorted[pos]];
-      const uint32_t k = min(min(64u, pf ? kBkWinPieces / pf : 64u), nreg - pos);
-      tiles[(uint64_t)blockIdx.x * kBkTilesMax + tt++] = bk_desc(pos, k, pf);
-      pos += k;
-    }
-    while (pos < nk) {
-      const uint32_t k = min(64u, nk - pos);
-      tiles[(uint64_t)blockIdx.x * kBkTilesMax + tt++] = bk_desc(pos, k, kBkLong);
-      pos += k;
-    }
-    while (tt < kBkTilesMax) tiles[(uint64_t)blockIdx.x * kBkTilesMax + tt++] = 0u;
-  }
-}
-
-// One wave's bucketed tile: gather, then (in this wave's turn) stage and hash.
-struct BkTile {
-  uint64_t key;   // this lane's key (valid: lane < K)
-  uint64_t a16;   // its first 16-B piece (absolute address)
-  uint32_t sh;    // key start within that piece
-  uint32_t len;
-  uint32_t K, P;  // wave-uniform
-  bool valid;
-};
-
-template <int OUT>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_span_bk(
-    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offsets, uint64_t off_base, uint64_t n,
-    uint64_t regions, const uint16_t* __restrict__ perm, const uint32_t* __restrict__ tiles, uint32_t seed,
-    Sink sink) {
-  static_assert(OUT != kOutProbe, "the probe's row registers would spill beside the held tile: k_span");
-  constexpr int kPieces = kSpanPiecesMax;  // 20 x 1 KiB fetches cover the 1276-piece window
-  extern __shared__ __attribute__((aligned(16))) uint32_t span_lds[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  // XCD-aware: blocks b and b + 8 share an XCD, so a region's workgroups are every 8th block
-  const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
-  const uint64_t r = (uint64_t)(slot / kBkWgsPerRegion) * 8u + xcd;
-  const uint32_t w = slot % kBkWgsPerRegion;
-  if (r >= regions) return;  // workgroup-uniform
-  const uint32_t* td = tiles + r * kBkTilesMax + 2u * w;
-  const uint32_t d0 = __builtin_amdgcn_readfirstlane(td[0]), d1 = __builtin_amdgcn_readfirstlane(td[1]);
-  if (((d0 | d1) >> 13) == 0u) return;  // both tiles empty: workgroup-uniform
-  const uint32_t d = wave ? d1 : d0;
-  BkTile ti;
-  ti.K = (d >> 13) & 0x7fu;
-  ti.P = d >> 20;
-  const uint32_t pos = d & 0x1fffu;
-  ti.valid = lane < ti.K;
-  const uint64_t k0 = r * kBkRegion;
-  uint64_t o0 = 0, o1 = 0;
-  if (ti.valid) {
-    ti.key = k0 + perm[k0 + pos + lane];
-    o0 = offsets[ti.key];
-    o1 = offsets[ti.key + 1];
-  } else {
-    ti.key = 0;
-  }
-  const uint64_t addr = reinterpret_cast<uintptr_t>(bytes) + (o0 - off_base);
-  ti.a16 = addr & ~(uint64_t)15;
-  ti.sh = (uint32_t)(addr & 15u);
-  ti.len = (uint32_t)(o1 - o0);
-  const bool staged = ti.K != 0 && ti.P <= kBkPmax;
-  if (staged) {
-    // gather: item idx = 64 q + lane is piece j of slot s (idx = s P + j); lanes past a key's
-    // pieces, or past the K slots, load nothing
-    const uint32_t P = ti.P ? ti.P : 1u;
-    const uint32_t pk = ti.valid && ti.len ? (ti.sh + ti.len + 15u) >> 4 : 0u;
-    const uint32_t alo = (uint32_t)ti.a16, ahi = (uint32_t)(ti.a16 >> 32);
-    const uint32_t dq = 64u / P, rq = 64u % P;
-    uint32_t s_ = lane / P, j = lane % P;
-    const uint32_t items = ti.K * ti.P;
-    u32x4 reg[kPieces];
-#pragma unroll
-    for (int q = 0; q < kPieces; ++q) {
-      reg[q] = u32x4{0u, 0u, 0u, 0u};
-      if ((uint32_t)q * 64u < items) {  // wave-uniform
-        const int src = (int)min(s_, 63u);
-        const uint32_t pks = (uint32_t)__shfl((int)pk, src);
-        const uint64_t as = (uint64_t)(uint32_t)__shfl((int)alo, src) | ((uint64_t)(uint32_t)__shfl((int)ahi, src) << 32);
-        if (s_ < ti.K && j < pks) reg[q] = *reinterpret_cast<g_u32x4*>(as + 16u * j);
-      }
-      s_ += dq;
-      j += rq;
-      if (j >= P) {
-        j -= P;
-        ++s_;
-      }
-    }
-    // wave 0 stages and hashes, one LDS-only barrier hands the window to wave 1 (k_span_pp)
-    for (uint32_t turn = 0; turn < 2; ++turn) {
-      if (turn) lds_barrier();
-      if (wave != turn) continue;
-#pragma unroll
-      for (int q = 0; q < kPieces; ++q)
-        if ((uint32_t)q * 64u + lane < items) reinterpret_cast<u32x4*>(span_lds)[64 * q + lane] = reg[q];
-      wave_lds_fence();
-      if (ti.valid) store_result<OUT>(sink, ti.key, hash_lds_u(span_lds, lane * ti.P * 16u + ti.sh, ti.len, seed));
-    }
-  } else {
-    lds_barrier();  // each wave passes one barrier
-    if (ti.valid) {  // keys over kBkPmax pieces or malformed: per lane from HBM
-      if (var_key_bad(o0, o1)) flag_bad_key(sink);
-      else store_result<OUT>(sink, ti.key, hash_bytes(bytes + (o0 - off_base), ti.len, seed));
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // Pieces (16 B) of every key staged per round by k_tiled. 8 (one 128-B line per
@@ -1319,37 +1135,9 @@ static hipError_t launch_fixed_t(const void* keys, uint32_t key_len, uint64_t n,
   return hipGetLastError();
 }
 
-// Bucketed spans: the plan into `scratch` (stream-ordered), then the hashing kernel.
-// scratch: n x 2 B of sorted indices (16-B aligned), then regions x kBkTilesMax x 4 B.
-size_t bucket_scratch_bytes(uint64_t n) {
-  const uint64_t regions = (n + kBkRegion - 1) / kBkRegion;
-  return (size_t)(((n * 2u + 15u) & ~(uint64_t)15) + regions * kBkTilesMax * 4u);
-}
-
-template <int OUT>
-static hipError_t launch_var_bucket(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                                    uint32_t seed, const Sink& sink, hipStream_t st, void* scratch) {
-  if constexpr (OUT == kOutProbe) {
-    return hipErrorInvalidValue;
-  } else {
-    const uint64_t regions = (n + kBkRegion - 1) / kBkRegion;
-    const uint64_t wgs = (regions + 7u) / 8u * 8u * kBkWgsPerRegion;
-    if (!scratch || regions > 0x7fffffffull || wgs > 0x7fffffffull) return hipErrorInvalidValue;
-    uint16_t* perm = reinterpret_cast<uint16_t*>(scratch);
-    uint32_t* tiles = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(scratch) + ((n * 2u + 15u) & ~(uint64_t)15));
-    hipLaunchKernelGGL(k_bucket_plan, dim3((unsigned)regions), dim3(kBkPlanThreads), 0, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, perm, tiles);
-    hipLaunchKernelGGL(k_span_bk<OUT>, dim3((unsigned)wgs), dim3(128), kSpanAlloc, st,
-                       reinterpret_cast<const uint8_t*>(bytes), offsets, off_base, n, regions, perm, tiles, seed, sink);
-    return hipGetLastError();
-  }
-}
-
 template <int OUT>
 static hipError_t launch_var_t(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
-                               uint32_t seed, const Sink& sink, hipStream_t st, int kernel, uint64_t key_bytes,
-                               void* scratch) {
-  if (kernel == kKernelBucket) return launch_var_bucket<OUT>(bytes, offsets, off_base, n, seed, sink, st, scratch);
+                               uint32_t seed, const Sink& sink, hipStream_t st, int kernel, uint64_t key_bytes) {
   // AUTO with a known byte count: the span kernel with a sized window up to a
   // mean key length of 300 B; beyond, 64-key spans overflow even 20 KiB and the
   // round kernel streams them (profiles/r1/sweep_var: U[8,2048] round 3797,
@@ -1388,15 +1176,15 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
 }
 
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
-                      const Sink& sink, int out_mode, hipStream_t st, int kernel, uint64_t key_bytes, void* scratch) {
+                      const Sink& sink, int out_mode, hipStream_t st, int kernel, uint64_t key_bytes) {
   if (n == 0) return hipSuccess;
   switch (out_mode) {
     case kOutHash:
-      return launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes, scratch);
+      return launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     case kOutUid:
-      return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes, scratch);
+      return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     default:
-      return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes, scratch);
+      return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
   }
 }
 

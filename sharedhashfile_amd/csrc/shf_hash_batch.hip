@@ -764,18 +764,7 @@ int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t 
   } else {
     k.status = c->d_status;
   }
-  if (kernel == shfhb::kKernelBucket) {
-    // the plan's scratch lives for this launch only, allocated and freed in the stream's order (so
-    // concurrent calls on other streams never share it)
-    void* scratch = nullptr;
-    HB_TRY(hipMallocAsync(&scratch, shfhb::bucket_scratch_bytes(n), st));
-    const hipError_t e = shfhb::launch_var(bytes, offsets, 0, n, seed, k, out_mode, st, kernel, key_bytes, scratch);
-    const hipError_t f = hipFreeAsync(scratch, st);
-    HB_TRY(e);
-    HB_TRY(f);
-  } else {
-    HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, k, out_mode, st, kernel, key_bytes));
-  }
+  HB_TRY(shfhb::launch_var(bytes, offsets, 0, n, seed, k, out_mode, st, kernel, key_bytes));
   if (sync) {
     HB_TRY(hipMemcpyAsync(c->h_status, k.status, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HB_TRY(hipStreamSynchronize(st));
@@ -786,7 +775,7 @@ int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t 
 
 bool var_kernel_valid(int kernel) {
   return kernel == SHF_HB_KERNEL_AUTO || kernel == SHF_HB_KERNEL_SPAN || kernel == SHF_HB_KERNEL_SPAN_PP ||
-         kernel == SHF_HB_KERNEL_GENERIC || kernel == SHF_HB_KERNEL_ROUND || kernel == SHF_HB_KERNEL_BUCKET;
+         kernel == SHF_HB_KERNEL_GENERIC || kernel == SHF_HB_KERNEL_ROUND;
 }
 
 // Can the forced fixed-length kernel take this shape? (AUTO always can.)

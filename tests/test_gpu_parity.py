@@ -46,7 +46,7 @@ def fixed_kernels(key_len, aligned=True):
     return ks
 
 
-VAR_KERNELS = [0, 3, 4, 5, 6, 7]  # AUTO, GENERIC, SPAN, ROUND, SPAN_PP, BUCKET
+VAR_KERNELS = [0, 3, 4, 5, 6]  # AUTO, GENERIC, SPAN, ROUND, SPAN_PP
 
 
 # ---------------------------------------------------------------------------
@@ -334,11 +334,11 @@ def test_var_long_keys_without_byte_count(hb, dev, oracle, lo, hi):
     data = rng.integers(0, 256, size=int(off[-1]) + 5, dtype=np.uint8)
     want = oracle.hash_var(data, off)
     d_data, d_o = d_u8(data, dev), d_off(off, dev)
-    for k in (0, 6, 7):
+    for k in (0, 6):
         assert np.array_equal(u64(hb.hash_var(d_data, d_o, kernel=k)), want), k
     # shifted start: every key unaligned
     d_o3 = d_off(off + np.uint64(3), dev)
-    for k in (6, 7):
+    for k in (6,):
         assert np.array_equal(u64(hb.hash_var(d_data, d_o3, kernel=k)), oracle.hash_var(data[3:], off)), k
 
 

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 SENTINEL = np.uint64(0xDEADBEEFDEADBEEF)
-VAR_KERNELS = [0, 3, 4, 5, 6, 7]  # AUTO, GENERIC, SPAN, ROUND, SPAN_PP, BUCKET
+VAR_KERNELS = [0, 3, 4, 5, 6]  # AUTO, GENERIC, SPAN, ROUND, SPAN_PP
 
 
 @pytest.fixture(scope="module")
