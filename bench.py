@@ -894,7 +894,8 @@ def cpu_baseline(args):
 # ---------------------------------------------------------------------------
 # rocprofv3 PMC passes (child processes, N=1 only): HBM bytes, VALU, waits
 # ---------------------------------------------------------------------------
-PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"],
+RDREQ = ["TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_sum"]
+PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"], RDREQ,
               ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                "GRBM_GUI_ACTIVE"]]
 PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b", "ceil_copynt_hot", "ceil_copynt_1b",
@@ -969,9 +970,10 @@ def collect_pmc(args, names):
             for c, v in cs.items():
                 res[w][c] = float(np.median(v))
     return res, ("per launch, median over the child's launches of each workload's kernel at its own grid size; "
-                 "configs 2/3 at <= 10M keys. traffic = FETCH_SIZE x the factor that turns the FETCH_SIZE of a "
-                 "same-run ceiling pattern of known bytes into those bytes (fetch_factor, fetch_factor_from) + "
-                 "WRITE_SIZE, KiB -> B. valu_busy = 4 x SQ_ACTIVE_INST_VALU / (%d SIMDs x GRBM_GUI_ACTIVE / %d XCDs) "
+                 "configs 2/3 at <= 10M keys. traffic = the bytes the L2s read from the fabric, from the 32/64/128-B "
+                 "read request counts (TCC_EA0_RDREQ_*B_sum; Infinity-Cache hits included), + WRITE_SIZE; "
+                 "traffic_fetch_calibrated = FETCH_SIZE x the factor that turns the FETCH_SIZE of a same-run "
+                 "ceiling pattern of known bytes into those bytes (fetch_factor, fetch_factor_from) + WRITE_SIZE. valu_busy = 4 x SQ_ACTIVE_INST_VALU / (%d SIMDs x GRBM_GUI_ACTIVE / %d XCDs) "
                  "(rocprof's VALUBusy formula); valu_busy_range = it divided by the same formula's reading on the "
                  "two VALU-saturating launches (half- and full-rate instructions): the kernel's true VALU "
                  "occupancy lies between. wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES" % (SIMDS, XCDS))
@@ -1001,12 +1003,31 @@ def pmc_calibration(pmc):
     return cal
 
 
+def read_bytes_by_size(c):
+    """Bytes the L2s requested from the fabric, from the per-size request counts
+    (32-, 64- and 128-B requests): exact for any access pattern, unlike
+    FETCH_SIZE (which tallies a 128-B request as 64 B). None without them."""
+    if all(c.get(k) is not None for k in RDREQ[:3]):
+        return 32.0 * c[RDREQ[0]] + 64.0 * c[RDREQ[1]] + 128.0 * c[RDREQ[2]]
+    return None
+
+
 def pmc_fields(c, algorithmic_bytes, fetch_factor=2.0, valu_sat=None):
-    """Derived counters of one workload (c: per-launch medians, KiB for the sizes)."""
+    """Derived counters of one workload (c: per-launch medians, KiB for the sizes).
+    traffic = the per-size read bytes + WRITE_SIZE when the request-size pass ran,
+    else FETCH_SIZE x the calibrated factor + WRITE_SIZE."""
     out = {}
-    if c.get("FETCH_SIZE") is not None and c.get("WRITE_SIZE") is not None:
-        t = (fetch_factor * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    rb = read_bytes_by_size(c)
+    if c.get("WRITE_SIZE") is not None and (rb is not None or c.get("FETCH_SIZE") is not None):
+        if c.get("FETCH_SIZE") is not None:
+            out["traffic_fetch_calibrated"] = (fetch_factor * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        t = rb + c["WRITE_SIZE"] * 1024.0 if rb is not None else out["traffic_fetch_calibrated"]
         out["traffic"] = t
+        out["traffic_from"] = "per-size read requests + WRITE_SIZE" if rb is not None else \
+            "FETCH_SIZE x fetch_factor + WRITE_SIZE"
+        if rb is not None:
+            out["read_bytes"] = rb
+            out["read_requests_32_64_128B"] = [c.get(k) for k in RDREQ[:3]]
         out["traffic_over_algorithmic"] = round(t / algorithmic_bytes, 4) if algorithmic_bytes else None
     v = valu_formula(c)
     if v is not None:
@@ -1089,7 +1110,8 @@ def roofline_of(name, r, results, pmc, cal, args):
         else:
             ro["traffic_at_pmc_size"] = f.get("traffic")
             ro["pmc_lanes"] = lanes
-        for k in ("traffic_over_algorithmic", "valu_busy", "valu_busy_range", "wait_frac"):
+        for k in ("traffic_over_algorithmic", "traffic_from", "traffic_fetch_calibrated", "read_bytes",
+                  "read_requests_32_64_128B", "valu_busy", "valu_busy_range", "wait_frac"):
             if k in f:
                 ro[k] = f[k]
     vr = ro.get("valu_busy_range")

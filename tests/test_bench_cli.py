@@ -76,6 +76,12 @@ def test_pmc_fields_and_limiter():
                           "GRBM_GUI_ACTIVE": 8.0, "SQ_WAIT_ANY": 30.0, "SQ_WAVE_CYCLES": 100.0}, 250 * 1024.0,
                          fetch_factor=2.0, valu_sat=[2.0, 4.0])
     assert f["traffic"] == 250 * 1024.0 and f["traffic_over_algorithmic"] == 1.0
+    assert f["traffic_from"].startswith("FETCH_SIZE")
+    # the per-size request counts win when present: 32/64/128-B requests, exact bytes
+    g = bench.pmc_fields({"FETCH_SIZE": 100.0, "WRITE_SIZE": 50.0, "TCC_EA0_RDREQ_32B_sum": 2.0,
+                          "TCC_EA0_RDREQ_64B_sum": 1.0, "TCC_EA0_RDREQ_128B_sum": 1600.0}, 1.0)
+    assert g["read_bytes"] == 32 * 2 + 64 + 128 * 1600 and g["traffic"] == g["read_bytes"] + 50 * 1024.0
+    assert g["traffic_fetch_calibrated"] == 250 * 1024.0
     assert f["valu_busy"] == 4.0 and f["valu_busy_range"] == [1.0, 2.0]
     assert f["wait_frac"] == 0.3
     assert bench.limiter(0.95, 0.5) == "hbm"
