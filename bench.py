@@ -1115,7 +1115,10 @@ def roofline_of(name, r, results, pmc, cal, args):
             if k in f:
                 ro[k] = f[k]
     vr = ro.get("valu_busy_range")
-    ro["limiter"] = limiter(ro.get("frac_of_copy_ceiling"), vr[1] if vr else ro.get("valu_busy"))
+    if name.startswith("ceil_"):
+        ro["limiter"] = "n/a (a ceiling line: what its access shape moves)"
+    else:
+        ro["limiter"] = limiter(ro.get("frac_of_copy_ceiling"), vr[1] if vr else ro.get("valu_busy"))
     return ro
 
 

@@ -68,7 +68,7 @@ def _worker(rank, world, port, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 8])
 def test_gloo_sharded_batch(world):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
