@@ -73,31 +73,32 @@ BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for 
 KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
                "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>",
                "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy(", "ceil_copy_hot": "k_ceil_copy(",
-               "ceil_copy_1b": "k_ceil_copy(", "ceil_read16": "k_ceil_read16<false>", "ceil_read16nt": "k_ceil_read16<true>", "ceil_gather128": "k_ceil_gather128",
+               "ceil_copy_1b": "k_ceil_copy(", "ceil_read16": "k_ceil_read16<false", "ceil_read16nt": "k_ceil_read16<true, 256",
+               "ceil_read16w1": "k_ceil_read16<true, 64", "ceil_gather128": "k_ceil_gather128",
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
                "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
                "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128"}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
-                  "ceil_read16", "ceil_read16nt", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
+                  "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
                   "ceil_valu_mul"]
 # the ceiling each hashing line is reported against: the best copy of the same bytes on the same buffers
 # (one lane per 16 B as k_fixed16 moves them, plain or nontemporal stores), measured in this run right after
 # the line
 CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copynt"], "fixed16_hot": ["ceil_copy_hot", "ceil_copynt_hot"],
-              "shard1b": ["ceil_copy_1b", "ceil_copynt_1b"], "fixed256": ["ceil_read16", "ceil_read16nt"],
-              "var": ["ceil_read16", "ceil_read16nt"],
+              "shard1b": ["ceil_copy_1b", "ceil_copynt_1b"], "fixed256": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
+              "var": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
               "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copynt"]}
 # timing order: each ceiling right after the line it bounds (same buffers, same thermal state)
 ORDER = ["fixed16", "ceil_copy", "ceil_copynt", "fixed16_hot", "ceil_copy_hot", "ceil_copynt_hot", "shard1b",
-         "ceil_copy_1b", "ceil_copynt_1b", "fixed256", "ceil_read16", "ceil_read16nt", "var", "probe16", "ceil_probe_rows",
+         "ceil_copy_1b", "ceil_copynt_1b", "fixed256", "ceil_read16", "ceil_read16nt", "ceil_read16w1", "var", "probe16", "ceil_probe_rows",
          "ceil_gather128", "tabpart", "ceil_stream16u", "ceil_valu_add", "ceil_valu_mul"]
 # the pattern whose known byte count calibrates each line's FETCH_SIZE
 FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
                 "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
                 "tabpart": "ceil_stream16u"}
 # bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
-CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copynt": 16, "ceil_read16": 256, "ceil_read16nt": 256,
+CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copynt": 16, "ceil_read16": 256, "ceil_read16nt": 256, "ceil_read16w1": 256,
                       "ceil_gather128": 132,
                       "ceil_stream16u": 16}
 VALU_ITERS = 2048          # rounds of 8 chained VALU ops per lane in the VALU-saturating launches
@@ -300,6 +301,8 @@ def _up(x, m):
 def grid_threads(name, n):
     """Work-items of one launch of workload `name` over n keys / lanes / jobs:
     rocprofv3's Grid_Size of that launch (the PMC rows are matched on it)."""
+    if name == "ceil_read16w1":
+        return n                        # one 64-thread workgroup per 64 lanes (n a multiple of 64)
     if name in ("fixed16", "fixed16_hot", "shard1b", "probe16") or name.startswith("ceil_"):
         return _up(n, 256)              # 256-thread blocks, one key / lane per thread
     if name == "fixed256":
@@ -521,7 +524,7 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
                            "order) fetched 8 lanes per row + 4-B index + 16-B store per lane, %d lanes" % n,
                            grid=grid_threads("ceil_probe_rows", n)))
         wl[-1].keep = (rows, rid, out)
-    if "ceil_read16" in only or "ceil_read16nt" in only:
+    if {"ceil_read16", "ceil_read16nt", "ceil_read16w1"} & set(only):
         n = read16_lanes(args, only)
         if "fixed256" in bufs:
             keys, out, _ = bufs["fixed256"]
@@ -530,7 +533,8 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
             keys = torch.empty(n * 256, dtype=torch.uint8, device=dev)
             out = torch.empty((n, 2), dtype=torch.int64, device=dev)
             where = "a buffer of its own"
-        for name, kind, st in (("ceil_read16", hb.CEIL_READ16, "plain"), ("ceil_read16nt", hb.CEIL_READ16_NT, "nt")):
+        for name, kind, st in (("ceil_read16", hb.CEIL_READ16, "plain"), ("ceil_read16nt", hb.CEIL_READ16_NT, "nt"),
+                               ("ceil_read16w1", hb.CEIL_READ16_W1, "nt, one wave per workgroup")):
             if name not in only:
                 continue
             wl.append(Workload(name, n, 272,
@@ -910,6 +914,7 @@ def pmc_child_sizes(args, want):
     sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
              "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
              "ceil_read16": read16_lanes(child, set(want)), "ceil_read16nt": read16_lanes(child, set(want)),
+             "ceil_read16w1": read16_lanes(child, set(want)),
              "ceil_gather128": args.keys16, "ceil_stream16u": 2 * args.keys16, "ceil_valu_add": VALU_LANES,
              "ceil_valu_mul": VALU_LANES}
     return {w: sizes[w] for w in want if w in sizes}, k256, kvar

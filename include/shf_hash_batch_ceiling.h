@@ -37,6 +37,7 @@ extern "C" {
 #define SHF_HB_CEIL_COPY_SLEEP 9 /* nontemporal loads, a short s_sleep before the store */
 #define SHF_HB_CEIL_COPY2 10     /* two 16-B units per lane */
 #define SHF_HB_CEIL_READ16_NT 11 /* SHF_HB_CEIL_READ16 with a nontemporal store */
+#define SHF_HB_CEIL_READ16_W1 12 /* SHF_HB_CEIL_READ16_NT launched one wave (64 lanes) per workgroup */
 
 /* Enqueue one launch on hip_stream. Device pointers; dst 16-B aligned, n x 16 B. */
 SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,

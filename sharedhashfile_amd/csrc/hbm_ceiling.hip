@@ -13,7 +13,9 @@
 //                    contiguous 16-KiB span, 1 KiB per instruction, the way k_tiled
 //                    and k_span stage a tile), their XOR stored as 16 B. 272 B per
 //                    lane: configs[2]'s 256 + 16 B per key (configs[3]: 284).
-//                    Plain or nontemporal store (the hashing kernels store nt).
+//                    Plain or nontemporal store (the hashing kernels store nt);
+//                    256-thread workgroups, or one wave per workgroup (k_tiled's
+//                    and k_span's launch shape).
 //   k_ceil_gather128 lane i: one 128-B row rows[idx[i]] (the row index read as a
 //                    4-B stream), fetched 8 lanes per row exactly as the probe's
 //                    row fetch does (probe_scan_coop), 16 B stored per lane. With
@@ -90,10 +92,10 @@ __global__ __launch_bounds__(kBlock) void k_ceil_copy4(const u32x4* __restrict__
     if (i0 + q * kBlock < n) dst[i0 + q * kBlock] = v[q];
 }
 
-template <bool NT_STORE>
-__global__ __launch_bounds__(kBlock) void k_ceil_read16(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                        uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+template <bool NT_STORE, uint32_t BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_ceil_read16(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   const uint64_t wave = i >> 6;
   const uint32_t lane = threadIdx.x & 63u;
   if (wave * 64u >= n) return;  // whole waves only: n is a multiple of 64 (checked by the launcher)
@@ -192,11 +194,17 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
     }
     case SHF_HB_CEIL_READ16:
     case SHF_HB_CEIL_READ16_NT:
+    case SHF_HB_CEIL_READ16_W1:
       if (!al16 || n % 64u || src_bytes < 256u * n) return SHF_HB_ERR_ARG;
       if (kind == SHF_HB_CEIL_READ16)
         hipLaunchKernelGGL(k_ceil_read16<false>, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
-      else
+      else if (kind == SHF_HB_CEIL_READ16_NT)
         hipLaunchKernelGGL(k_ceil_read16<true>, grid, block, 0, st, (const u32x4*)d_src, (u32x4*)d_dst, n);
+      else if (n / 64u > 0x7fffffffull)
+        return SHF_HB_ERR_ARG;
+      else  // one wave per workgroup: k_tiled's launch shape
+        hipLaunchKernelGGL((k_ceil_read16<true, 64>), dim3((unsigned)(n / 64u)), dim3(64), 0, st,
+                           (const u32x4*)d_src, (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_GATHER128:
       // every idx[i] must name a row inside src: checked by the caller's construction (a permutation

@@ -106,6 +106,7 @@ def test_grid_threads_match_the_launchers():
     assert bench.grid_threads("var", 65) == 128
     assert bench.grid_threads("tabpart", 1024) == 1024 * 512
     assert bench.grid_threads("ceil_read16", 64) == 256
+    assert bench.grid_threads("ceil_read16w1", 128) == 128
     assert bench.grid_threads("ceil_copynt", 10_000_000) == 10_000_128
 
 

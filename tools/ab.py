@@ -178,8 +178,10 @@ def main():
     for k, ts in times.items():
         ts = sorted(ts)
         med = ts[len(ts) // 2]
-        print("%-12s median %8.3f ms  min %8.3f ms  %7.1f GB/s  %6.2f Gkeys/s" % (
-            k, med, ts[0], n * per_key / med / 1e6, n / med / 1e6))
+        what = "M tabs/s" if a.workload == "tab" else "G keys/s"
+        rate = n / med / (1e3 if a.workload == "tab" else 1e6)
+        print("%-12s median %8.3f ms  min %8.3f ms  %7.1f GB/s  %6.2f %s" % (
+            k, med, ts[0], n * per_key / med / 1e6, rate, what))
 
 
 if __name__ == "__main__":
