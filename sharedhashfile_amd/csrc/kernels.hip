@@ -963,11 +963,23 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
       span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
     }
   } else {
-    const bool over = has && !bad;  // span over the window: streamed through it in rounds, in this wave's turn
-    uint8_t* win = reinterpret_cast<uint8_t*>(span_lds);
-    if (wave == 0 && over) vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, win);
+    // A span over the window is streamed in rounds through this wave's half of
+    // it (the round path needs kVrLdsBytes). Wave 0 goes first; wave 1 waits for
+    // the hand-over only if wave 0 may be staging a span in the whole window,
+    // i.e. unless wave 0's tile is itself over the window (its bytes alone
+    // exceed it) -- then both stream at once, as k_vround's independent waves do.
+    const bool over = has && !bad;
+    uint8_t* win = reinterpret_cast<uint8_t*>(span_lds) + wave * kVrLdsBytes;
+    bool first = wave == 0;
+    if (wave == 1 && over) {
+      const uint64_t s0 = offsets[(t - 1) * 64u];  // wave 0's tile: keys [64 (t - 1), 64 t)
+      const uint64_t e0 = pack64(__builtin_amdgcn_readfirstlane((uint32_t)raw.o0),
+                                 __builtin_amdgcn_readfirstlane((uint32_t)(raw.o0 >> 32)));
+      first = e0 < s0 || e0 - s0 > cap;  // decreasing: wave 0 flags its keys and stages nothing
+    }
+    if (first && over) vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, win);
     lds_barrier();
-    if (wave == 1 && over) vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, win);
+    if (!first && over) vround_tile<OUT>(bytes, ti.key, ti.valid, ti.start, ti.len, seed, sink, win);
     if (has && bad) span_tile_from_hbm<OUT>(bytes, off_base, n, raw, lane, seed, sink);
   }
 }
@@ -1023,7 +1035,8 @@ constexpr uint32_t kLdsPerCu = 160u * 1024u;
 template <int OUT>
 static hipError_t launch_var_span_pingpong(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n,
                                            uint32_t seed, const Sink& sink, hipStream_t st) {
-  static_assert(kSpanAlloc - kSpanPad >= kVrLdsBytes, "the window holds the round fallback's LDS");
+  static_assert(kSpanAlloc - kSpanPad >= 2u * kVrLdsBytes && kVrLdsBytes % 16u == 0,
+                "the window holds two waves' round fallback LDS");
   const uint64_t tiles = (n + 63) / 64;
   const uint64_t wgs = (tiles + 1) / 2;
   if (wgs > 0x7fffffffull) return hipErrorInvalidValue;

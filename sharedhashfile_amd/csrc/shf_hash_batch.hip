@@ -264,8 +264,26 @@ int ensure_probe_staging(DevCtx* c) {
   return SHF_HB_OK;
 }
 
+// Pages this library page-locks for the length of one call
+// (host_fixed_pageable_zero_copy). Another thread's call over the same caller
+// buffer neither locks them again (PageLock::lock refuses any overlap) nor
+// takes them for the caller's own page-locked memory (is_host_pinned), which
+// would have its copies or kernel still reading them over PCIe when the first
+// call unlocks them. An entry is made before the pages are locked and removed
+// after they are unlocked, so a lookup that sees them locked always finds it.
+std::mutex g_lib_lock_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_lib_locks;  // [start, end)
+
+bool library_locked(const void* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> g(g_lib_lock_mu);
+  for (const auto& r : g_lib_locks)
+    if (a >= r.first && a < r.second) return true;
+  return false;
+}
+
 // Caller host memory that is already page-locked (hipHostMalloc /
-// hipHostRegister): DMA straight from / into it, no staging copy.
+// hipHostRegister by the caller): DMA straight from / into it, no staging copy.
 bool is_host_pinned(const void* p) {
   if (!p) return false;
   hipPointerAttribute_t a;
@@ -273,7 +291,7 @@ bool is_host_pinned(const void* p) {
     (void)hipGetLastError();  // pageable memory: clear the sticky error
     return false;
   }
-  return a.type == hipMemoryTypeHost;
+  return a.type == hipMemoryTypeHost && !library_locked(p);
 }
 
 // memcpy split over a few threads (SHF_HB_COPY_THREADS, default 8, read per
@@ -477,7 +495,7 @@ uint32_t zero_copy_max_key() {
 // Device address of host bytes [p, p + bytes), when they lie in one
 // page-locked allocation that the current device maps; else nullptr.
 void* host_range_device_ptr(const void* p, size_t bytes) {
-  if (!p || !bytes) return nullptr;
+  if (!p || !bytes || library_locked(p)) return nullptr;  // another call's pages: not the caller's to use
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   void* d = nullptr;
@@ -513,9 +531,20 @@ HostJob hash_job(shf_hash128* out);
 struct PageLock {
   void* p = nullptr;
   void* dev = nullptr;
+  std::pair<uintptr_t, uintptr_t> range{0, 0};  // listed in g_lib_locks while non-empty
   bool lock(void* at, size_t bytes) {
+    const std::pair<uintptr_t, uintptr_t> r{reinterpret_cast<uintptr_t>(at), reinterpret_cast<uintptr_t>(at) + bytes};
+    {
+      // pages another call of this library holds: leave them to it (concurrent hipHostRegister
+      // of one range, and unlocking under the other call's kernel, are both avoided)
+      std::lock_guard<std::mutex> g(g_lib_lock_mu);
+      for (const auto& o : g_lib_locks)
+        if (r.first < o.second && o.first < r.second) return false;
+      g_lib_locks.push_back(r);
+    }
+    range = r;
     if (hipHostRegister(at, bytes, hipHostRegisterMapped) != hipSuccess) {
-      (void)hipGetLastError();
+      (void)hipGetLastError();  // e.g. pages another call (or the caller) has locked: not ours to use
       return false;
     }
     p = at;
@@ -527,6 +556,11 @@ struct PageLock {
   }
   ~PageLock() {
     if (p && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+    if (range.second) {  // after the unlock (equal entries of other calls are interchangeable)
+      std::lock_guard<std::mutex> g(g_lib_lock_mu);
+      const auto it = std::find(g_lib_locks.begin(), g_lib_locks.end(), range);
+      if (it != g_lib_locks.end()) g_lib_locks.erase(it);
+    }
   }
 };
 
