@@ -74,10 +74,10 @@ KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1
                "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>",
                "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy(", "ceil_copy_hot": "k_ceil_copy(",
                "ceil_copy_1b": "k_ceil_copy(", "ceil_read16": "k_ceil_read16<false", "ceil_read16nt": "k_ceil_read16<true, 256",
-               "ceil_read16w1": "k_ceil_read16<true, 64", "ceil_gather128": "k_ceil_gather128",
+               "ceil_read16w1": "k_ceil_read16<true, 64", "ceil_gather128": "k_ceil_gather128<false>",
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
                "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
-               "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128"}
+               "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128<true>"}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
                   "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
@@ -517,13 +517,15 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
     if "ceil_probe_rows" in only and "probe_rows" in bufs:
         rows, rid, n = bufs["probe_rows"]
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
-        wl.append(Workload("ceil_probe_rows", n, 148,
-                           [ceil_launcher(hb, hb.CEIL_GATHER128, rows.data_ptr(), rows.numel(), rid.data_ptr(),
-                                          out.data_ptr(), n, dev)], "k_ceil_gather128",
-                           "probe16's own row reads without the hash: each key's 128-B row (its slot and row, in key "
-                           "order) fetched 8 lanes per row + 4-B index + 16-B store per lane, %d lanes" % n,
-                           grid=grid_threads("ceil_probe_rows", n)))
-        wl[-1].keep = (rows, rid, out)
+        rid16 = torch.zeros((n, 4), dtype=torch.int32, device=dev)  # the row in the first word of a 16-B record
+        rid16[:, 0] = rid
+        wl.append(Workload("ceil_probe_rows", n, 160,
+                           [ceil_launcher(hb, hb.CEIL_PROBE_ROWS, rows.data_ptr(), rows.numel(), rid16.data_ptr(),
+                                          out.data_ptr(), n, dev)], "k_ceil_gather128<true>",
+                           "probe16's own row reads without the hash: a 16-B record per lane naming its key's 128-B "
+                           "row (slot and row, in key order), the row fetched 8 lanes per row, a 16-B nt store: the "
+                           "probe's 160 B per key, %d lanes" % n, grid=grid_threads("ceil_probe_rows", n)))
+        wl[-1].keep = (rows, rid16, out)
     if {"ceil_read16", "ceil_read16nt", "ceil_read16w1"} & set(only):
         n = read16_lanes(args, only)
         if "fixed256" in bufs:

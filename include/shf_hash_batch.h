@@ -201,12 +201,17 @@ typedef struct shf_row_index shf_row_index; /* opaque; lives on the device curre
 SHF_HB_API int shf_row_index_create(uint64_t n_slots, shf_row_index **out);
 SHF_HB_API int shf_row_index_destroy(shf_row_index *index);
 /* Copy SHF_ROW_INDEX_TABS entries (host or device memory) into the index
- * (entries naming a slot >= n_slots are treated as absent by the probes). */
+ * (entries naming a slot >= n_slots are treated as absent by the probes).
+ * Synchronous; it also makes the probes' compact copy of the map (a 1-B rank
+ * per entry among its window's distinct entries, plus those entries: 768 KiB
+ * that stay in L2 where the 2-MiB map does not). */
 SHF_HB_API int shf_row_index_set_tabs(shf_row_index *index, const uint32_t *tab_slot);
 /* Copy count row blocks (count * 64 KiB, host or device memory) into slots
  * [first, first + count). Synchronous. */
 SHF_HB_API int shf_row_index_set_rows(shf_row_index *index, uint64_t first, uint64_t count, const void *rows);
-/* Device pointers of the index, for producers that fill it on the device. */
+/* Device pointers of the index, for producers that fill it on the device.
+ * From this call on the probes read tab_slot itself (the compact copy made by
+ * set_tabs could go stale), so device-side writes are seen by the next probe. */
 SHF_HB_API int shf_row_index_device_ptrs(const shf_row_index *index, uint32_t **d_tab_slot, void **d_rows,
                                          uint64_t *n_slots);
 

@@ -116,6 +116,7 @@ CEIL_COPY_SLEEP = 9
 CEIL_COPY2 = 10
 CEIL_READ16_NT = 11
 CEIL_READ16_W1 = 12
+CEIL_PROBE_ROWS = 13
 
 
 def load(path=None):

@@ -110,12 +110,20 @@ __global__ __launch_bounds__(BLOCK) void k_ceil_read16(const u32x4* __restrict__
   else dst[i] = x;
 }
 
+// IDX16: the index arrives as 16-B records (the row index in the first word), as
+// the probe reads a 16-B key per lane, and the result is stored nontemporally as
+// the probe stores its record: SHF_HB_CEIL_PROBE_ROWS, 160 B per lane.
+template <bool IDX16>
 __global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __restrict__ rows,
                                                            const uint32_t* __restrict__ idx, u32x4* __restrict__ dst,
                                                            uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t r = i < n ? __builtin_nontemporal_load(&idx[i]) : 0u;  // lanes past n fetch row 0 and discard it
+  uint32_t r = 0;  // lanes past n fetch row 0 and discard it
+  if (i < n) {
+    if constexpr (IDX16) r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(idx) + i).x;
+    else r = __builtin_nontemporal_load(&idx[i]);
+  }
   u32x4 g[8];
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
@@ -125,7 +133,10 @@ __global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __rest
   u32x4 x = g[0];
 #pragma unroll
   for (int q = 1; q < 8; ++q) x ^= g[q];
-  if (i < n) dst[i] = x;
+  if (i < n) {
+    if constexpr (IDX16) __builtin_nontemporal_store(x, &dst[i]);
+    else dst[i] = x;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_ceil_stream16u(const uint8_t* __restrict__ src, u32x4* __restrict__ dst,
@@ -207,10 +218,16 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
                            (const u32x4*)d_src, (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_GATHER128:
+    case SHF_HB_CEIL_PROBE_ROWS:
       // every idx[i] must name a row inside src: checked by the caller's construction (a permutation
-      // of src_bytes / 128 rows), not here -- the launcher cannot read device memory
+      // of src_bytes / 128 rows, or the probe's own rows), not here -- the launcher cannot read device memory
       if (!al16 || !d_idx || src_bytes < 128u || src_bytes / 128u > 0xffffffffull) return SHF_HB_ERR_ARG;
-      hipLaunchKernelGGL(k_ceil_gather128, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
+      if (kind == SHF_HB_CEIL_GATHER128)
+        hipLaunchKernelGGL(k_ceil_gather128<false>, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
+      else if ((reinterpret_cast<uintptr_t>(d_idx) & 15u) != 0)
+        return SHF_HB_ERR_ARG;
+      else
+        hipLaunchKernelGGL(k_ceil_gather128<true>, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_STREAM16U: {
       const uint32_t shift = (uint32_t)(((uintptr_t)d_src) & 15u) ? 0u : 7u;  // aligned base: read 7 bytes in

@@ -29,6 +29,8 @@ struct Sink {
   const uint32_t* tab_slot = nullptr;  // kOutProbe: row index, see shf_hash_batch.h
   const uint8_t* rows = nullptr;
   uint64_t n_slots = 0;
+  const uint8_t* map8 = nullptr;       // kOutProbe: compact copy of tab_slot (launch_compact_map), or null
+  const uint32_t* win_tab = nullptr;
   uint32_t* status = nullptr;  // variable-length keys: set to 1 when a key's offsets are invalid
 };
 
@@ -48,6 +50,14 @@ hipError_t launch_status_take(uint32_t* word, uint32_t* taken, hipStream_t st);
 
 // Row pre-probe of precomputed hashes (n x 16 B on device) into sink.out.
 hipError_t launch_probe_hashes(const void* hashes, uint64_t n, const Sink& sink, hipStream_t st);
+
+// Compact copy of a row index's tab_slot map for the probes: map8[(win << 11) | tab2]
+// = the entry's rank among its window's distinct indexed entries (0..253), 254 = not
+// indexed (SHF_PROBE_NONE or a slot >= n_slots), 255 = a window with more than 254
+// distinct entries (read tab_slot itself); win_tab[(win << 8) | rank] = the entry.
+constexpr uint32_t kMapRanks = 254, kMapNone = 254, kMapEscape = 255;
+hipError_t launch_compact_map(const uint32_t* tab_slot, uint64_t n_slots, uint8_t* map8, uint32_t* win_tab,
+                              hipStream_t st);
 
 // Tab part / shrink copy (tab_copy.hip): one workgroup per job, every pointer on device.
 hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint64_t dst_bytes, shf_tab_job* jobs,

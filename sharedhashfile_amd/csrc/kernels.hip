@@ -66,6 +66,9 @@ struct ProbeLoc {
   uint32_t win, tab2, row, want, e;
 };
 
+// The map entry comes from the compact map when the index has one (512 KiB of
+// ranks + the windows' distinct entries, which stay in L2 beside the row stream
+// where the 2-MiB tab_slot map did not: +20 % at 10M keys, profiles/r3/ab_mapsize.txt).
 __device__ __forceinline__ ProbeLoc probe_locate(const Sink& k, const State& s) {
   ProbeLoc p;
   const uint32_t lo = (uint32_t)s.h1;
@@ -73,7 +76,16 @@ __device__ __forceinline__ ProbeLoc probe_locate(const Sink& k, const State& s) 
   p.tab2 = (lo >> 16) & 0x7ffu;
   p.row = (uint32_t)(s.h1 >> 32) & 0x1ffu;
   p.want = p.tab2 | (((uint32_t)s.h2 & 0x1fffffu) << 11);
-  p.e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.tab_slot))[(p.win << 11) | p.tab2];
+  const uint32_t at = (p.win << 11) | p.tab2;
+  if (k.map8) {
+    const uint32_t r = reinterpret_cast<const __attribute__((address_space(1))) uint8_t*>(
+        reinterpret_cast<uintptr_t>(k.map8))[at];
+    if (r < kMapRanks) p.e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.win_tab))[(p.win << 8) | r];
+    else if (r == kMapNone) p.e = kProbeNone;
+    else p.e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.tab_slot))[at];
+  } else {
+    p.e = reinterpret_cast<g_u32*>(reinterpret_cast<uintptr_t>(k.tab_slot))[at];
+  }
   return p;
 }
 
@@ -1207,6 +1219,72 @@ __global__ __launch_bounds__(64) void k_status_take(uint32_t* word, uint32_t* ta
 
 hipError_t launch_status_take(uint32_t* word, uint32_t* taken, hipStream_t st) {
   hipLaunchKernelGGL(k_status_take, dim3(1), dim3(64), 0, st, word, taken);
+  return hipGetLastError();
+}
+
+// One workgroup per window: its 2048 entries' distinct indexed values are
+// inserted into an LDS hash table, ranked in table order (a block scan), and
+// each entry is replaced by its value's rank.
+constexpr uint32_t kMapTable = 4096;  // >= 2 x 2048: open addressing stays short
+
+__global__ __launch_bounds__(256) void k_compact_map(const uint32_t* __restrict__ tab_slot, uint64_t n_slots,
+                                                     uint8_t* __restrict__ map8, uint32_t* __restrict__ win_tab) {
+  __shared__ uint32_t key[kMapTable];
+  __shared__ uint32_t rank[kMapTable];
+  __shared__ uint32_t wsum[4];
+  const uint32_t win = blockIdx.x, t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  for (uint32_t i = t; i < kMapTable; i += 256) key[i] = kProbeNone;
+  __syncthreads();
+  uint32_t e[8];
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) {
+    e[j] = tab_slot[(win << 11) + j * 256u + t];
+    if (e[j] != kProbeNone && (uint64_t)(e[j] >> 11) >= n_slots) e[j] = kProbeNone;  // not indexed
+    if (e[j] == kProbeNone) continue;
+    for (uint32_t h = (e[j] * 0x9e3779b1u) >> 20;; h = (h + 1) & (kMapTable - 1)) {
+      const uint32_t old = atomicCAS(&key[h], kProbeNone, e[j]);
+      if (old == kProbeNone || old == e[j]) break;
+    }
+  }
+  __syncthreads();
+  // ranks in table order: thread t owns table entries [16 t, 16 t + 16)
+  uint32_t cnt = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) cnt += key[16 * t + i] != kProbeNone;
+  uint32_t incl = cnt;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t r = incl - cnt;
+  for (uint32_t w = 0; w < wave; ++w) r += wsum[w];
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint32_t h = 16 * t + i;
+    if (key[h] == kProbeNone) continue;
+    rank[h] = r;
+    if (r < kMapRanks) win_tab[(win << 8) + r] = key[h];
+    ++r;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) {
+    uint32_t m = kMapNone;
+    if (e[j] != kProbeNone) {
+      uint32_t h = (e[j] * 0x9e3779b1u) >> 20;
+      while (key[h] != e[j]) h = (h + 1) & (kMapTable - 1);
+      m = rank[h] < kMapRanks ? rank[h] : kMapEscape;
+    }
+    map8[(win << 11) + j * 256u + t] = (uint8_t)m;
+  }
+}
+
+hipError_t launch_compact_map(const uint32_t* tab_slot, uint64_t n_slots, uint8_t* map8, uint32_t* win_tab,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(k_compact_map, dim3(256), dim3(256), 0, st, tab_slot, n_slots, map8, win_tab);
   return hipGetLastError();
 }
 

@@ -33,6 +33,12 @@ struct shf_row_index {
   uint32_t* d_tab_slot = nullptr;
   uint8_t* d_rows = nullptr;
   uint64_t n_slots = 0;
+  // the probes' compact copy of tab_slot (kernels.h launch_compact_map), made by set_tabs;
+  // not used once the device pointers were handed out (tab_slot may then change under it)
+  uint8_t* d_map8 = nullptr;
+  uint32_t* d_win_tab = nullptr;
+  bool compact = false;
+  mutable bool external = false;
 };
 
 namespace {
@@ -411,6 +417,10 @@ void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k,
     k->out = c->d_probe[s];
     k->hash_out = job.hash ? c->d_out[s] : nullptr;
     k->tab_slot = job.index->d_tab_slot;
+    if (job.index->compact && !job.index->external) {
+      k->map8 = job.index->d_map8;
+      k->win_tab = job.index->d_win_tab;
+    }
     k->rows = job.index->d_rows;
     k->n_slots = job.index->n_slots;
     *mode = shfhb::kOutProbe;
@@ -841,6 +851,10 @@ int probe_sink(const shf_row_index* index, void* d_probe, void* d_hashes, shfhb:
   sink->tab_slot = index->d_tab_slot;
   sink->rows = index->d_rows;
   sink->n_slots = index->n_slots;
+  if (index->compact && !index->external) {
+    sink->map8 = index->d_map8;
+    sink->win_tab = index->d_win_tab;
+  }
   return SHF_HB_OK;
 }
 
@@ -1023,6 +1037,8 @@ int shf_row_index_create(uint64_t n_slots, shf_row_index** out) {
   if (e == hipSuccess) e = hipMemset(x->d_tab_slot, 0xff, SHF_ROW_INDEX_TABS * sizeof(uint32_t));
   if (e == hipSuccess && n_slots) e = hipMalloc((void**)&x->d_rows, n_slots * SHF_ROW_INDEX_SLOT_BYTES);
   if (e == hipSuccess && n_slots) e = hipMemset(x->d_rows, 0, n_slots * SHF_ROW_INDEX_SLOT_BYTES);
+  if (e == hipSuccess) e = hipMalloc((void**)&x->d_map8, SHF_ROW_INDEX_TABS);
+  if (e == hipSuccess) e = hipMalloc((void**)&x->d_win_tab, 256u * 256u * sizeof(uint32_t));
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     (void)shf_row_index_destroy(x);
@@ -1039,6 +1055,8 @@ int shf_row_index_destroy(shf_row_index* index) {
   (void)hipSetDevice(index->dev);
   if (index->d_tab_slot) (void)hipFree(index->d_tab_slot);
   if (index->d_rows) (void)hipFree(index->d_rows);
+  if (index->d_map8) (void)hipFree(index->d_map8);
+  if (index->d_win_tab) (void)hipFree(index->d_win_tab);
   (void)hipSetDevice(prev);
   delete index;
   return SHF_HB_OK;
@@ -1046,7 +1064,16 @@ int shf_row_index_destroy(shf_row_index* index) {
 
 int shf_row_index_set_tabs(shf_row_index* index, const uint32_t* tab_slot) {
   if (!index || !tab_slot) return SHF_HB_ERR_ARG;
+  index->compact = false;
   HB_TRY(hipMemcpy(index->d_tab_slot, tab_slot, SHF_ROW_INDEX_TABS * sizeof(uint32_t), hipMemcpyDefault));
+  int prev = 0;
+  HB_TRY(hipGetDevice(&prev));
+  HB_TRY(hipSetDevice(index->dev));  // the compact copy is made on the index's device
+  hipError_t e = shfhb::launch_compact_map(index->d_tab_slot, index->n_slots, index->d_map8, index->d_win_tab, nullptr);
+  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+  (void)hipSetDevice(prev);
+  HB_TRY(e);
+  index->compact = true;
   return SHF_HB_OK;
 }
 
@@ -1060,6 +1087,7 @@ int shf_row_index_set_rows(shf_row_index* index, uint64_t first, uint64_t count,
 
 int shf_row_index_device_ptrs(const shf_row_index* index, uint32_t** d_tab_slot, void** d_rows, uint64_t* n_slots) {
   if (!index) return SHF_HB_ERR_ARG;
+  index->external = true;  // the caller may now write tab_slot: the probes read it directly
   if (d_tab_slot) *d_tab_slot = index->d_tab_slot;
   if (d_rows) *d_rows = index->d_rows;
   if (n_slots) *n_slots = index->n_slots;

@@ -146,6 +146,51 @@ def test_probe_ragged_index(torch, oracle):
         empty.close()
 
 
+def test_probe_compact_map_ranks_escapes_and_device_writes(torch, oracle):
+    """The probes read a compact copy of tab_slot that set_tabs makes (a rank per
+    entry among its window's distinct entries + the windows' entry lists). Windows
+    with 254 distinct entries (every rank used), 255 (one escape to tab_slot) and
+    2048 (mostly escapes), then writes through the device pointers, which the
+    probes must see at once (they then read tab_slot itself)."""
+    import ctypes
+
+    n = 200_000
+    keys = np.frombuffer(splitmix_bytes(n * 16, 91), dtype=np.uint8).reshape(n, 16)
+    h = oracle.hash_fixed(keys)
+    tab_slot, rows, n_slots, _ = synthetic_index(h, tabs_per_win=2)
+    ts = tab_slot.copy().reshape(256, 2048)
+    slot = ts >> np.uint32(11)
+    t2 = np.arange(2048, dtype=np.uint32)
+    ts[0] = (slot[0] << np.uint32(11)) | t2                      # 2048 distinct: ranks 0..253, then escapes
+    ts[1] = (slot[1] << np.uint32(11)) | (t2 % np.uint32(254))   # exactly 254 distinct
+    ts[2] = (slot[2] << np.uint32(11)) | (t2 % np.uint32(255))   # 255: one value escapes
+    ts[3, ::3] = NONE                                            # some entries unindexed
+    ts = ts.reshape(-1)
+    idx = hb.RowIndex(n_slots, ts, rows)
+    try:
+        d = _dev(torch, keys)
+        for kernel in (hb.KERNEL_FIXED16, hb.KERNEL_GENERIC):
+            rec = hb.probe_fixed(idx, d, kernel=kernel)
+            torch.cuda.synchronize()
+            assert np.array_equal(_u32(rec), oracle.probe(h, ts, rows)), kernel
+        # writes through the device pointers (a producer filling the index on the device)
+        d_ts, _, _ = idx.device_ptrs()
+        ts2 = ts.copy().reshape(256, 2048)
+        ts2[4:8] = NONE
+        ts2[9] = ts2[10]
+        ts2 = ts2.reshape(-1)
+        src = torch.from_numpy(ts2.view(np.int32)).to("cuda")
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        torch.cuda.synchronize()
+        assert hip.hipMemcpy(d_ts, src.data_ptr(), ts2.nbytes, 3) == 0  # hipMemcpyDeviceToDevice
+        rec = hb.probe_fixed(idx, d)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u32(rec), oracle.probe(h, ts2, rows))
+    finally:
+        idx.close()
+
+
 def test_probe_full_size_config_b(torch, oracle):
     """configs[1] shape (10M x 16 B) with a device-built index: GPU hashes and
     probes agree across kernels; a 20 000-key sample agrees with the oracle."""
