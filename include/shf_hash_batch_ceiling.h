@@ -39,7 +39,8 @@ extern "C" {
 #define SHF_HB_CEIL_READ16_NT 11 /* SHF_HB_CEIL_READ16 with a nontemporal store */
 #define SHF_HB_CEIL_READ16_W1 12 /* SHF_HB_CEIL_READ16_NT launched one wave (64 lanes) per workgroup */
 #define SHF_HB_CEIL_PROBE_ROWS 13 /* SHF_HB_CEIL_GATHER128 with the index as 16-B records (row in the first word,
-                                     d_idx 16-B aligned) and a nontemporal store: the probe's 160 B per lane */
+                                     d_idx 16-B aligned), a nontemporal store and the probe kernel's 32 KiB of LDS
+                                     per workgroup (its occupancy): the probe's 160 B per lane */
 
 /* Enqueue one launch on hip_stream. Device pointers; dst 16-B aligned, n x 16 B. */
 SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,

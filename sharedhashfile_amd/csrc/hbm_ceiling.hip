@@ -226,8 +226,9 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
         hipLaunchKernelGGL(k_ceil_gather128<false>, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
       else if ((reinterpret_cast<uintptr_t>(d_idx) & 15u) != 0)
         return SHF_HB_ERR_ARG;
-      else
-        hipLaunchKernelGGL(k_ceil_gather128<true>, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
+      else  // with the probe kernel's 32 KiB of LDS per 256-thread workgroup, hence its occupancy
+        hipLaunchKernelGGL(k_ceil_gather128<true>, grid, block, 32u * 1024u, st, (const uint8_t*)d_src, d_idx,
+                           (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_STREAM16U: {
       const uint32_t shift = (uint32_t)(((uintptr_t)d_src) & 15u) ? 0u : 7u;  // aligned base: read 7 bytes in
