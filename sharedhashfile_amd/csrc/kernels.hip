@@ -669,19 +669,30 @@ __device__ __forceinline__ u32x4 lds_read16(const uint32_t* lds, uint32_t byte) 
   return *(lds_u32x4_a1*)((lds_u8*)lds + byte);  // generic -> LDS address space (lds is an LDS pointer)
 }
 
-__device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
-  const uint32_t nblocks = len >> 4;
-  State s{seed, seed};
-  // software pipeline: block j's chain beside block j+1's mixes and block j+2's read
-  // (the compiler folds this loop-carried read into one read at the point of
-  // use; forcing it a block ahead, or a two-block-deep pipeline with block
-  // j+2's mixes beside block j's chain, measured no faster in k_span or
-  // k_span_pp: profiles/r2/ab_span/ab_pipe, ab_deep)
-  u32x4 cur = lds_read16(lds, p);
+// Hash `len` bytes at byte offset p of the staged span with one unaligned
+// ds_read_b128 per block, in two parts split at the last LDS read: the body
+// blocks (hash_lds_u_blocks: the state, and the tail's 16 bytes in `cur`),
+// then the register-only tail and finalisation (hash_tail_finish), so a
+// window can be handed on between them.
+// Software pipeline: block j's chain beside block j+1's mixes and block j+2's
+// read (the compiler folds this loop-carried read into one read at the point
+// of use; forcing it a block ahead, or a two-block-deep pipeline with block
+// j+2's mixes beside block j's chain, measured no faster in k_span or
+// k_span_pp: profiles/r2/ab_span/ab_pipe, ab_deep). The read address is the
+// loop counter (one VALU add and one compare per block).
+__device__ __forceinline__ void hash_lds_u_blocks(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed,
+                                                  State& s, u32x4& cur) {
+  s = State{seed, seed};
+  cur = lds_read16(lds, p);
   u32x4 nxt = lds_read16(lds, p + 16u);
   uint64_t m1 = mix_k1(pack64(cur.x, cur.y)), m2 = mix_k2(pack64(cur.z, cur.w));
-  for (uint32_t j = 0; j < nblocks; ++j) {
-    const u32x4 nn = lds_read16(lds, p + 16u * j + 32u);
+  // a: the LDS address of nxt
+  uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>((lds_u8*)lds + p + 16u);
+  const uint32_t end = a + (len & ~15u);
+  while (a != end) {
+    a += 16u;
+    asm("" : "+v"(a));  // keeps the address the only induction variable (LSR would add a counter)
+    const u32x4 nn = *(lds_u32x4_a1*)(lds_u8*)(uintptr_t)a;
     const uint64_t n1 = mix_k1(pack64(nxt.x, nxt.y)), n2 = mix_k2(pack64(nxt.z, nxt.w));
     chain_block(s, m1, m2);
     m1 = n1;
@@ -689,6 +700,9 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
     cur = nxt;
     nxt = nn;
   }
+}
+
+__device__ __forceinline__ void hash_tail_finish(State& s, const u32x4& cur, uint32_t len) {
   const uint32_t rem = len & 15u;
   if (rem) {  // cur holds the tail's bytes
     const uint64_t t1 = pack64(cur.x, cur.y) & low_bytes_mask(rem);
@@ -696,6 +710,13 @@ __device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uin
     tail_block(s, t1, t2, rem);
   }
   finish(s, len);
+}
+
+__device__ __forceinline__ State hash_lds_u(const uint32_t* lds, uint32_t p, uint32_t len, uint32_t seed) {
+  State s;
+  u32x4 cur;
+  hash_lds_u_blocks(lds, p, len, seed, s, cur);
+  hash_tail_finish(s, cur, len);
   return s;
 }
 
@@ -966,9 +987,26 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
     if (wave == 0) {
       span_stage<PIECES>(span_lds, reg, ti.span16, lane);
       wave_lds_fence();
-      span_hash_tile<OUT>(span_lds, bytes, ti, seed, sink);
+      // the body blocks only: the tail and fmix run after the hand-over, from
+      // registers (the state parks in reg[0..1], dead on this wave once staged,
+      // so no register is live across the barrier beyond the held span).
+      // U[8,512] +1.1-1.5 %, all-260 B +0.9-3.2 %, U[64,448] +0.7-1.6 %
+      // (profiles/r3/ab_early_handover*.txt)
+      if (ti.valid) {
+        State s;
+        u32x4 cur;
+        hash_lds_u_blocks(span_lds, (uint32_t)(reinterpret_cast<uintptr_t>(bytes) + ti.start - ti.base), ti.len,
+                          seed, s, cur);
+        reg[0] = u32x4{(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
+        reg[1] = cur;
+      }
     }
-    lds_barrier();  // wave 0 is done with the window (its result stores may still be in flight)
+    lds_barrier();  // wave 0 has read the window for the last time
+    if (wave == 0 && ti.valid) {
+      State s{pack64(reg[0].x, reg[0].y), pack64(reg[0].z, reg[0].w)};
+      hash_tail_finish(s, reg[1], ti.len);
+      store_result<OUT>(sink, ti.key, s);
+    }
     if (wave == 1) {
       span_stage<PIECES>(span_lds, reg, ti.span16, lane);
       wave_lds_fence();
