@@ -70,3 +70,25 @@ def test_two_rank_rehearsal_shards_configs4():
     assert set(line["slowest_over_fastest_rank"]) == {"fixed16", "shard1b"}
     assert all(v >= 1.0 for v in line["slowest_over_fastest_rank"].values())
     assert line["barrier_backend"] == "gloo"
+
+
+def test_two_rank_rehearsal_under_torch_distributed_run():
+    """The driver's launcher (`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`):
+    the ranks come from the launcher's environment, not from bench.py's own spawn."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2"]
+    p = subprocess.run(cmd + ARGS + ["--allow-shared-gpu"], capture_output=True, text=True, timeout=300, env=_env(),
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0's line only
+    line = json.loads(lines[0])
+    assert line["ranks"] == 2 and line["verified"] is True
+    assert line["secondary"]["shard1b"]["shards"] == [[0, 500_000_000], [500_000_000, 1_000_000_000]]
+    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
+    assert line["barrier_backend"] == "gloo"
