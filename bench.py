@@ -77,8 +77,9 @@ KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1
                "ceil_read16w1": "k_ceil_read16<true, 64", "ceil_gather128": "k_ceil_gather128<false>",
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
                "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
-               "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128<true>"}
-HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart"]
+               "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128<true>",
+               "winorder": "k_wo_scatter"}
+HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart", "winorder"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
                   "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
                   "ceil_valu_mul"]
@@ -88,15 +89,16 @@ CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot"
 CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copynt"], "fixed16_hot": ["ceil_copy_hot", "ceil_copynt_hot"],
               "shard1b": ["ceil_copy_1b", "ceil_copynt_1b"], "fixed256": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
               "var": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
-              "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copynt"]}
+              "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copynt"],
+              "winorder": ["ceil_copy", "ceil_copynt"]}
 # timing order: each ceiling right after the line it bounds (same buffers, same thermal state)
 ORDER = ["fixed16", "ceil_copy", "ceil_copynt", "fixed16_hot", "ceil_copy_hot", "ceil_copynt_hot", "shard1b",
          "ceil_copy_1b", "ceil_copynt_1b", "fixed256", "ceil_read16", "ceil_read16nt", "ceil_read16w1", "var", "probe16", "ceil_probe_rows",
-         "ceil_gather128", "tabpart", "ceil_stream16u", "ceil_valu_add", "ceil_valu_mul"]
+         "ceil_gather128", "tabpart", "ceil_stream16u", "winorder", "ceil_valu_add", "ceil_valu_mul"]
 # the pattern whose known byte count calibrates each line's FETCH_SIZE
 FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
                 "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
-                "tabpart": "ceil_stream16u"}
+                "tabpart": "ceil_stream16u", "winorder": "ceil_copy"}
 # bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
 CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copynt": 16, "ceil_read16": 256, "ceil_read16nt": 256, "ceil_read16w1": 256,
                       "ceil_gather128": 132,
@@ -311,6 +313,8 @@ def grid_threads(name, n):
         return ((n + 63) // 64 + 1) // 2 * 128  # k_span_pp: one 128-thread workgroup per two tiles
     if name == "tabpart":
         return n * 512                  # k_tab_split: one 512-thread workgroup per tab
+    if name == "winorder":
+        return ((n + 4095) // 4096 + 3) // 4 * 256  # k_wo_scatter: 4 waves per workgroup, a 4096-key chunk each
     return None
 
 
@@ -462,6 +466,8 @@ def make_workloads(args, dev, rank, world=1):
         wl.append(w)
     if "tabpart" in only:
         wl.append(tab_workload(args, dev, seed_base))
+    if "winorder" in only:
+        wl.append(win_order_workload(args, dev, seed_base))
     wl += ceiling_workloads(args, dev, only, bufs, fixed16_pairs)
     torch.cuda.synchronize()
     return sorted(wl, key=lambda w: ORDER.index(w.name) if w.name in ORDER else len(ORDER))
@@ -583,6 +589,47 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
         if not hasattr(w, "unit"):
             w.unit = "lanes/s"
     return wl
+
+
+def win_order_workload(args, dev, seed_base):
+    """Window order (SURVEY.md §8 f1's use; shf_win_order_async): the key
+    indices of 10M hash records stably sorted by h1 & 0xff. Algorithmic bytes
+    per key: the 16-B record read once + the 4-B index written (20 B); the
+    library's passes add one window byte written and read per key."""
+    import ctypes
+
+    import torch
+
+    import sharedhashfile_amd as hb
+    from sharedhashfile_amd.keygen import device_random_bytes
+
+    n = args.keys16
+    hashes = device_random_bytes(n * 16, seed_base + 7, dev).view(torch.int64).view(n, 2)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    start = torch.empty(257, dtype=torch.int32, device=dev)
+    lib = hb.load()
+    ws = torch.empty(lib.shf_win_order_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    fn = lib.shf_win_order_async
+    argv = (ctypes.c_void_p(hashes.data_ptr()), ctypes.c_uint64(n), ctypes.c_void_p(perm.data_ptr()),
+            ctypes.c_void_p(start.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()),
+            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+
+    def launch():
+        rc = fn(*argv)
+        if rc:
+            raise hb.ShfHashBatchError(rc, "shf_win_order_async")
+
+    def verify():
+        from oracle.oracle_py import Oracle
+
+        want_p, want_s = Oracle.win_order(hashes.cpu().numpy().view(np.uint64))
+        ok = (np.array_equal(perm.cpu().numpy().view(np.uint32), want_p) and
+              np.array_equal(start.cpu().numpy().view(np.uint32), want_s))
+        return bool(ok), int(n)
+
+    return Workload("winorder", n, 16 + 4, [launch], "k_wo_hist + k_wo_scan + k_wo_scatter",
+                    "%d 16-B hash records ordered by window (stable counting sort, 3 launches)" % n, verify,
+                    grid_threads("winorder", n))
 
 
 def tab_workload(args, dev, seed_base):
@@ -914,7 +961,7 @@ def pmc_child_sizes(args, want):
     k256, kvar = min(args.keys256, 10_000_000), min(args.keysvar, 10_000_000)
     child = argparse.Namespace(keys256=k256, keys16=args.keys16)
     sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
-             "tabpart": args.tab_jobs, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
+             "tabpart": args.tab_jobs, "winorder": args.keys16, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
              "ceil_read16": read16_lanes(child, set(want)), "ceil_read16nt": read16_lanes(child, set(want)),
              "ceil_read16w1": read16_lanes(child, set(want)),
              "ceil_gather128": args.keys16, "ceil_stream16u": 2 * args.keys16, "ceil_valu_add": VALU_LANES,

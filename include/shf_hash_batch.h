@@ -45,6 +45,7 @@
 #ifndef SHF_HASH_BATCH_H
 #define SHF_HASH_BATCH_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -302,6 +303,32 @@ SHF_HB_API int shf_tab_copy_batch(const void *src, uint64_t src_bytes, void *dst
  * memory, shf.c:683-692): of the entries naming tab_old, every second one
  * (the 2nd, 4th, ...) now names tab_new. */
 SHF_HB_API int shf_tab_part_redirect(uint16_t *map, uint32_t tab_old, uint32_t tab_new);
+
+/* ---- window order of a batch ("sorting a batch by win") ---
+ *
+ * perm[0..n) = the key indices 0..n-1 stably sorted by the window each key's
+ * hash selects, win = h1 & 0xff (the put/get bit consumer,
+ * /root/reference/src/shf.c:800, :893): window 0's keys first, each window's
+ * keys in batch order. win_start (optional, 257 entries) = the position in
+ * perm of each window's first key, then n.
+ * Everything a put/get/del touches belongs to its key's window (the window's
+ * lock, tab2 -> tab map, tabs and tab files; new tabs are numbered per window,
+ * shf.c:432), so running a batch's puts/gets/dels in perm order leaves the
+ * store byte for byte as batch order does, uids included, while consecutive
+ * operations find their window's structures in cache (INTEGRATION.md §8;
+ * shf_put_batch_var_win_ordered in shf_hash_batch_shf.h).
+ * n < 2^32 (32-bit indices); n == 0 sets win_start to zeros.
+ *
+ * _async: every pointer on the device, enqueued on hip_stream; d_workspace of
+ * at least shf_win_order_workspace_bytes(n) bytes, in use until the call has
+ * run on the stream. Not reentrant on one workspace.
+ * shf_win_order: synchronous; mem = SHF_HASH_MEM_DEVICE (device pointers) or
+ * SHF_HASH_MEM_HOST (host pointers, copied through device buffers). */
+SHF_HB_API size_t shf_win_order_workspace_bytes(uint64_t n);
+SHF_HB_API int shf_win_order_async(const shf_hash128 *d_hashes, uint64_t n, uint32_t *d_perm,
+                                   uint32_t *d_win_start, void *d_workspace, size_t workspace_bytes,
+                                   void *hip_stream);
+SHF_HB_API int shf_win_order(const shf_hash128 *hashes, uint64_t n, uint32_t *perm, uint32_t *win_start, int mem);
 
 /* ---- status of asynchronous variable-length calls -------------------------
  * Waits for hip_stream (NULL = the null stream), then returns SHF_HB_ERR_ARG if

@@ -15,6 +15,11 @@
  *   shf_get_batch_probed()   INTEGRATION.md §6: a get batch driven by row
  *                            pre-probe records, falling back to the ordinary
  *                            get with the batch hash
+ *   shf_put_batch_var_win_ordered(), shf_get_batch_win_ordered()
+ *                            the same put / get loops run in
+ *                            the GPU's window order (shf_win_order): the store
+ *                            ends byte for byte as in batch order, each
+ *                            window's structures are met while in cache
  *
  * Include it after the reference's shf.private.h and shf.h, in that order
  * (shf.h names the types shf.private.h defines). Everything is static inline:
@@ -119,6 +124,62 @@ static inline uint64_t shf_get_batch_probed(SHF *shf, const char *bytes, const u
         }
     }
     if (fast) *fast = f;
+    return found;
+}
+
+/* shf_put_batch_var() in window order: one GPU batch hash, the GPU's window
+ * order of those hashes (shf_win_order), then shf_put_key_val() per key in
+ * that order. Keys of one window keep their batch order and windows share no
+ * state, so the store (files, uids) ends exactly as shf_put_batch_var() leaves
+ * it. Returns n, the number of puts made before the first one that did not
+ * return SHF_RET_KEY_PUT (in window order: which keys went in is then
+ * perm[0 .. returned)), or a negative SHF_HB_ERR_* status with nothing put.
+ * perm_out (optional, n entries): the order used. */
+static inline int64_t shf_put_batch_var_win_ordered(SHF *shf, const char *bytes, const uint64_t *offsets, uint64_t n,
+                                                    const char *vals, const uint64_t *val_offsets,
+                                                    uint32_t *perm_out)
+{
+    if (n == 0) return 0;
+    shf_hash128 *h = (shf_hash128 *)malloc(n * sizeof *h);
+    uint32_t *perm = perm_out ? perm_out : (uint32_t *)malloc(n * sizeof *perm);
+    if (!h || !perm) {
+        free(h);
+        if (!perm_out) free(perm);
+        return SHF_HB_ERR_NOMEM;
+    }
+    int rc = shf_hash_batch_var(bytes, offsets, n, SHF_HASH_BATCH_SEED, h, SHF_HASH_MEM_HOST);
+    if (rc == SHF_HB_OK) rc = shf_win_order(h, n, perm, NULL, SHF_HASH_MEM_HOST);
+    uint64_t j = 0;
+    if (rc == SHF_HB_OK)
+        for (; j < n; ++j) {
+            const uint64_t i = perm[j];
+            shf_use_hash(bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]), &h[i]);
+            if (shf_put_key_val(shf, vals + val_offsets[i], (uint32_t)(val_offsets[i + 1] - val_offsets[i])) !=
+                SHF_RET_KEY_PUT)
+                break;
+        }
+    free(h);
+    if (!perm_out) free(perm);
+    return rc == SHF_HB_OK ? (int64_t)j : rc;
+}
+
+/* Get n keys with their batch hashes in window order (perm from shf_win_order
+ * of those hashes): shf_get_key_val_copy() per key, on_found(ctx, i) with the
+ * key's batch index i for every key found (shf_val / shf_val_len hold its
+ * value then). Returns the keys found. */
+static inline uint64_t shf_get_batch_win_ordered(SHF *shf, const char *bytes, const uint64_t *offsets, uint64_t n,
+                                                 const shf_hash128 *hashes, const uint32_t *perm,
+                                                 void (*on_found)(void *ctx, uint64_t i), void *ctx)
+{
+    uint64_t found = 0;
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint64_t i = perm[j];
+        shf_use_hash(bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]), &hashes[i]);
+        if (shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND) {
+            ++found;
+            if (on_found) on_found(ctx, i);
+        }
+    }
     return found;
 }
 

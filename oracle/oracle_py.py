@@ -110,6 +110,17 @@ class Oracle:
             raise ValueError("oracle_tab_split: output does not fit")
         return keep, move
 
+    @staticmethod
+    def win_order(hashes):
+        """(perm, win_start): the key indices stably sorted by win = h1 & 0xff
+        (shf.c:800), and each window's first position, then n (numpy)."""
+        h = np.ascontiguousarray(hashes, dtype=np.uint64).reshape(-1, 2)
+        win = (h[:, 0] & np.uint64(0xFF)).astype(np.int64)
+        perm = np.argsort(win, kind="stable").astype(np.uint32)
+        start = np.zeros(257, dtype=np.uint32)
+        start[1:] = np.cumsum(np.bincount(win, minlength=256))
+        return perm, start
+
     def smhasher(self):
         return self.lib.oracle_smhasher_verification()
 
@@ -138,6 +149,9 @@ def reference_lib():
     lib.ref_store_get_plain.restype = ctypes.c_int64
     lib.ref_store_get_probed.argtypes = [vp, vp, vp, u64, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)]
     lib.ref_store_get_probed.restype = ctypes.c_int64
+    lib.ref_put_in_order.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, vp, vp, vp, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    lib.ref_put_in_order.restype = ctypes.c_int64
     lib.ref_part_capture.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, u32, u32, u32, u32,
                                      ctypes.c_char_p]
     lib.ref_part_capture.restype = ctypes.c_int64
@@ -203,3 +217,38 @@ def reference_part_capture(data, offsets, fixed_key_len=0, fixed_val_len=0, fact
                         "map_after": maps[2048:].copy(), "before": rd("before"), "old": rd("old"),
                         "new": rd("new")})
         return res
+
+
+def reference_put_in_order(data, offsets, hashes, order, folder, name, lockable=1):
+    """The reference's own put loop over keys order[0..n) with the given hashes
+    (oracle/ref_export.c ref_put_in_order), into a fresh store folder/name that
+    stays on disk. order None = batch order. Returns (found, uids, put_seconds,
+    get_seconds)."""
+    lib = reference_lib()
+    if lib is None:
+        raise RuntimeError("oracle/_ref/libref_shf.so not built")
+    data = np.ascontiguousarray(data).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    hashes = np.ascontiguousarray(hashes, dtype=np.uint64)
+    n = offsets.size - 1
+    uids = np.zeros(n, dtype=np.uint32)
+    order = None if order is None else np.ascontiguousarray(order, dtype=np.uint32)
+    ps, gs = ctypes.c_double(), ctypes.c_double()
+    found = lib.ref_put_in_order(folder.encode(), name.encode(), data.ctypes.data, offsets.ctypes.data, n,
+                                 hashes.ctypes.data, order.ctypes.data if order is not None else None,
+                                 uids.ctypes.data, lockable, ctypes.byref(ps), ctypes.byref(gs))
+    if found < 0:
+        raise RuntimeError("ref_put_in_order failed (%d)" % found)
+    return found, uids, ps.value, gs.value
+
+
+def store_files(folder, name):
+    """{relative path: bytes} of every file of store folder/name (<name>.shf/...)."""
+    root = os.path.join(folder, name + ".shf")
+    out = {}
+    for d, _, files in os.walk(root):
+        for f in files:
+            p = os.path.join(d, f)
+            with open(p, "rb") as fh:
+                out[os.path.relpath(p, root)] = fh.read()
+    return out

@@ -293,3 +293,50 @@ int64_t ref_part_capture(const char *folder, const char *name, const uint8_t *by
     (void)shf_del(shf);
     return caps;
 }
+
+/* ---- window order (shf_win_order): one batch put in a given order ---------
+ * Keys order[0..n) (key i = bytes[offsets[i] .. offsets[i+1]), value: i as 8
+ * bytes) are put with the supplied hashes (2 x u64 per key, the seam of
+ * test.9.shf.c:176-182) into a fresh store folder/name; uids[i] = the shf_uid
+ * the put of key i left (shf.c:852). Then every key is read back in the same
+ * order (shf_get_key_val_copy) and checked. The store is detached, not
+ * deleted: its files stay for the caller to compare. put_seconds /
+ * get_seconds: the two loops' wall time. Returns the keys found with their
+ * value (n when all went in), or < 0 (-1: store, -2: a put failed). */
+int64_t ref_put_in_order(const char *folder, const char *name, const uint8_t *bytes, const uint64_t *offsets,
+                         uint64_t n, const uint64_t *hashes, const uint32_t *order, uint32_t *uids, int lockable,
+                         double *put_seconds, double *get_seconds)
+{
+    shf_init();
+    SHF *shf = shf_attach(folder, name, 0);
+    if (!shf) return -1;
+    shf_set_is_lockable(shf, (uint32_t)lockable);
+    double t0 = ref_now();
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint64_t i = order ? order[j] : j;
+        shf_hash.u64[0] = hashes[2 * i];
+        shf_hash.u64[1] = hashes[2 * i + 1];
+        shf_hash_key = (const char *)bytes + offsets[i];
+        shf_hash_key_len = (uint32_t)(offsets[i + 1] - offsets[i]);
+        if (shf_put_key_val(shf, (const char *)&i, sizeof(i)) != SHF_RET_KEY_PUT) {
+            shf_detach(shf);
+            return -2;
+        }
+        uids[i] = shf_uid;
+    }
+    double t1 = ref_now();
+    int64_t good = 0;
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint64_t i = order ? order[j] : j;
+        shf_hash.u64[0] = hashes[2 * i];
+        shf_hash.u64[1] = hashes[2 * i + 1];
+        shf_hash_key = (const char *)bytes + offsets[i];
+        shf_hash_key_len = (uint32_t)(offsets[i + 1] - offsets[i]);
+        good += shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND && ref_val_is(i);
+    }
+    double t2 = ref_now();
+    if (put_seconds) *put_seconds = t1 - t0;
+    if (get_seconds) *get_seconds = t2 - t1;
+    shf_detach(shf);
+    return good;
+}

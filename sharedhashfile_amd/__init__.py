@@ -94,6 +94,9 @@ _SIGS = {
     "shf_tab_copy_batch_async": [_VP, _U64, _VP, _U64, _VP, _U32, _VP, _U32, _VP, _VP],
     "shf_tab_copy_batch": [_VP, _U64, _VP, _U64, _VP, _U32, _VP, _U32, _VP, _INT],
     "shf_tab_part_redirect": [_VP, _U32, _U32],
+    "shf_win_order_workspace_bytes": [_U64],
+    "shf_win_order_async": [_VP, _U64, _VP, _VP, _VP, ctypes.c_size_t, _VP],
+    "shf_win_order": [_VP, _U64, _VP, _VP, _INT],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
@@ -119,6 +122,10 @@ CEIL_READ16_W1 = 12
 CEIL_PROBE_ROWS = 13
 
 
+_RESTYPES = {"shf_hash_batch_strerror": ctypes.c_char_p, "shf_hash_batch_version": ctypes.c_char_p,
+             "shf_win_order_workspace_bytes": ctypes.c_size_t}
+
+
 def load(path=None):
     """Load the C-ABI library (raises loudly when it is not built)."""
     global _lib
@@ -139,7 +146,7 @@ def load(path=None):
                 raise RuntimeError("%s does not export %s: rebuild it" % (p, name))
             continue  # an older variant loaded side by side for an A/B (tools/ab.py)
         fn.argtypes = args
-        fn.restype = ctypes.c_char_p if name in ("shf_hash_batch_strerror", "shf_hash_batch_version") else ctypes.c_int
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
     if path is None:
         _lib = lib
     return lib
@@ -150,7 +157,7 @@ def header_functions(header=HEADER_PATH):
     import re
 
     txt = open(header).read()
-    return sorted(set(re.findall(r"SHF_HB_API\s+(?:const\s+char\s*\*|int)\s*(shf_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"SHF_HB_API\s+(?:const\s+char\s*\*|int|size_t)\s*(shf_\w+)\s*\(", txt)))
 
 
 def _check(rc, where):
@@ -460,6 +467,47 @@ def probe_hashes(index, hashes, out=None, stream=None):
                                                  ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_probe_batch_hashes_async")
     return out
+
+
+def win_order(hashes, perm=None, win_start=None, workspace=None, stream=None):
+    """Window order of (n, 2) int64/uint64 CUDA hashes (shf_win_order_async):
+    returns (perm, win_start), int32 CUDA tensors of n and 257 entries (the
+    indices are unsigned 32-bit: view them as such past 2^31 keys)."""
+    import torch
+
+    _require_cuda(hashes, "hashes", _offset_dtypes())
+    if hashes.dim() != 2 or hashes.shape[1] != 2:
+        raise ValueError("hashes must have shape (n, 2)")
+    n = hashes.shape[0]
+    dev = hashes.device
+    if perm is None:
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+    _require_out(perm, (n,), (torch.int32,), dev)
+    if win_start is None:
+        win_start = torch.empty(257, dtype=torch.int32, device=dev)
+    _require_out(win_start, (257,), (torch.int32,), dev)
+    lib = load()
+    need = lib.shf_win_order_workspace_bytes(n)
+    if workspace is None:
+        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    _require_cuda_u8(workspace, "workspace")
+    with _on(hashes):
+        rc = lib.shf_win_order_async(ctypes.c_void_p(hashes.data_ptr()), n, ctypes.c_void_p(perm.data_ptr()),
+                                     ctypes.c_void_p(win_start.data_ptr()), ctypes.c_void_p(workspace.data_ptr()),
+                                     workspace.numel(), _stream_handle(stream))
+    _check(rc, "shf_win_order_async")
+    return perm, win_start
+
+
+def win_order_host(hashes):
+    """Host (n, 2) uint64 hashes in, host (perm uint32[n], win_start uint32[257]) out (shf_win_order)."""
+    h = np.ascontiguousarray(hashes, dtype=np.uint64).reshape(-1, 2)
+    n = h.shape[0]
+    perm = np.empty(n, dtype=np.uint32)
+    ws = np.empty(257, dtype=np.uint32)
+    rc = load().shf_win_order(h.ctypes.data, n, perm.ctypes.data, ws.ctypes.data, MEM_HOST)
+    _check(rc, "shf_win_order")
+    return perm, ws
 
 
 def probe_fixed_host(index, keys, key_len=None, seed=SEED, hashes=False):

@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libshf_hash_batch.so")
-SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip", "hbm_ceiling.hip"]
+SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip", "hbm_ceiling.hip", "win_order.hip"]
 HEADERS = ["kernels.h", "murmur3_mix.h"]
 ARCH = "gfx950"
 

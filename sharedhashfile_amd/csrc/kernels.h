@@ -64,4 +64,11 @@ hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint
                             uint32_t n_jobs, const uint16_t* maps, uint32_t n_maps, const shf_tab_params& prm,
                             hipStream_t st);
 
+// Window order (win_order.hip): perm = the batch's key indices stably sorted by
+// h1 & 0xff of their 16-B hash records; win_start (257 entries, optional) = the
+// first position of each window in perm, then n. workspace: win_order_workspace_bytes(n).
+uint64_t win_order_workspace_bytes(uint64_t n);
+hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
+                            hipStream_t st);
+
 }  // namespace shfhb

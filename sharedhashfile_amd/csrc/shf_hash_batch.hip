@@ -1221,6 +1221,50 @@ int shf_tab_copy_batch(const void* src, uint64_t src_bytes, void* dst, uint64_t 
   return SHF_HB_OK;
 }
 
+size_t shf_win_order_workspace_bytes(uint64_t n) { return (size_t)shfhb::win_order_workspace_bytes(n); }
+
+int shf_win_order_async(const shf_hash128* d_hashes, uint64_t n, uint32_t* d_perm, uint32_t* d_win_start,
+                        void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+  if (n == 0 && !d_win_start) return SHF_HB_OK;
+  if (n > 0xffffffffull) return SHF_HB_ERR_ARG;
+  if (n && (!d_hashes || !d_perm || !d_workspace || workspace_bytes < shfhb::win_order_workspace_bytes(n)))
+    return SHF_HB_ERR_ARG;
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  HB_TRY(shfhb::launch_win_order(d_hashes, n, d_perm, d_win_start, d_workspace, (hipStream_t)hip_stream));
+  return SHF_HB_OK;
+}
+
+int shf_win_order(const shf_hash128* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, int mem) {
+  if (mem != SHF_HASH_MEM_DEVICE && mem != SHF_HASH_MEM_HOST) return SHF_HB_ERR_ARG;
+  if (n == 0 && !win_start) return SHF_HB_OK;
+  if (n > 0xffffffffull || (n && (!hashes || !perm))) return SHF_HB_ERR_ARG;
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  hipStream_t st = c->st[0];
+  const size_t ws = (size_t)shfhb::win_order_workspace_bytes(n), ws_start = 257u * sizeof(uint32_t);
+  TmpDevBuf d_ws, d_h, d_p, d_s;
+  HB_TRY(hipMalloc(&d_ws.p, ws));
+  if (mem == SHF_HASH_MEM_DEVICE) {
+    HB_TRY(shfhb::launch_win_order(hashes, n, perm, win_start, d_ws.p, st));
+    HB_TRY(hipStreamSynchronize(st));
+    return SHF_HB_OK;
+  }
+  if (n) {
+    HB_TRY(hipMalloc(&d_h.p, n * sizeof(shf_hash128)));
+    HB_TRY(hipMalloc(&d_p.p, n * sizeof(uint32_t)));
+    HB_TRY(hipMemcpyAsync(d_h.p, hashes, n * sizeof(shf_hash128), hipMemcpyHostToDevice, st));
+  }
+  if (win_start) HB_TRY(hipMalloc(&d_s.p, ws_start));
+  HB_TRY(shfhb::launch_win_order(d_h.p, n, (uint32_t*)d_p.p, (uint32_t*)d_s.p, d_ws.p, st));
+  if (n) HB_TRY(hipMemcpyAsync(perm, d_p.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (win_start) HB_TRY(hipMemcpyAsync(win_start, d_s.p, ws_start, hipMemcpyDeviceToHost, st));
+  HB_TRY(hipStreamSynchronize(st));
+  return SHF_HB_OK;
+}
+
 int shf_tab_part_redirect(uint16_t* map, uint32_t tab_old, uint32_t tab_new) {
   if (!map || tab_old >= 2048u || tab_new >= 2048u || tab_old == tab_new) return SHF_HB_ERR_ARG;
   bool second = false;  // shf.c:683-692: the 1st, 3rd, ... stay, the 2nd, 4th, ... move

@@ -176,11 +176,54 @@ int main(int argc, char **argv)
     }
     if (ffound != nf) return fail("fixed keys: reference get after GPU-hashed put");
 
+    /* 5. the same batch put in the GPU's window order into a second store:
+     *    identical uids (the put loop leaves shf_uid) and every tab file equal */
+    SHF *wshf = shf_attach(folder, "seamwin", 0);
+    if (!wshf) return fail("shf_attach window order");
+    uint32_t *perm = malloc(n_put * sizeof *perm);
+    if (shf_put_batch_var_win_ordered(wshf, bytes, off, n_put, vals, voff, perm) != (int64_t)n_put)
+        return fail("shf_put_batch_var_win_ordered");
+    for (uint64_t j = 1; j < n_put; ++j) /* windows ascending, batch order inside each */
+        if ((h[perm[j]].h1 & 0xff) < (h[perm[j - 1]].h1 & 0xff) ||
+            ((h[perm[j]].h1 & 0xff) == (h[perm[j - 1]].h1 & 0xff) && perm[j] < perm[j - 1]))
+            return fail("window order: not a stable sort by window");
+    uint64_t same_files = 0;
+    for (uint32_t win = 0; win < SHF_WINS_PER_SHF; ++win) {
+        if (shf->shf_mmap->wins[win].tabs_used != wshf->shf_mmap->wins[win].tabs_used)
+            return fail("window order: tab counts differ");
+        for (uint32_t tab = 0; tab < shf->shf_mmap->wins[win].tabs_used; ++tab) {
+            char pa[512], pb[512];
+            snprintf(pa, sizeof pa, "%s/seam.shf/%03u/%04u.tab", folder, win, tab);
+            snprintf(pb, sizeof pb, "%s/seamwin.shf/%03u/%04u.tab", folder, win, tab);
+            FILE *fa = fopen(pa, "rb"), *fb = fopen(pb, "rb");
+            if (!fa || !fb) return fail("window order: tab file missing");
+            int ca, cb;
+            do {
+                ca = fgetc(fa);
+                cb = fgetc(fb);
+            } while (ca == cb && ca != EOF);
+            fclose(fa);
+            fclose(fb);
+            if (ca != cb) return fail("window order: tab files differ");
+            ++same_files;
+        }
+    }
+    /* a get batch (stored and absent keys) in window order gives the reference's answers */
+    shf_hash128 *hw = malloc(n * sizeof *hw);
+    uint32_t *permq = malloc(n * sizeof *permq);
+    memcpy(hw, h, n * sizeof *hw);
+    if (shf_win_order(hw, n, permq, NULL, SHF_HASH_MEM_HOST) != SHF_HB_OK) return fail("shf_win_order");
+    good_values = 0;
+    const uint64_t wfound2 = shf_get_batch_win_ordered(wshf, bytes, off, n, h, permq, check_value, NULL);
+    if (wfound2 != ref_found || good_values != ref_right) return fail("window-ordered get: answers differ");
+
     printf("{\"n_put\": %llu, \"n_query\": %llu, \"ref_found\": %llu, \"ref_right\": %llu, \"probed_found\": %llu, "
-           "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu}\n",
+           "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu, \"win_order_same_tab_files\": %llu, "
+           "\"win_order_found\": %llu}\n",
            (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
            (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
-           (unsigned long long)ffound);
+           (unsigned long long)ffound, (unsigned long long)same_files, (unsigned long long)wfound2);
+    shf_detach(wshf);
     /* the stores' files go with the folder (shf_del would run `du` and `rm` through popen) */
     shf_detach(shf);
     shf_detach(fshf);

@@ -160,7 +160,7 @@ def test_missing_library_raises(tmp_path):
         hbmod.load(str(tmp_path / "nope.so"))
 
 
-@pytest.mark.parametrize("source,min_kernels", [("kernels.hip", 30), ("tab_copy.hip", 1), ("hbm_ceiling.hip", 4)])
+@pytest.mark.parametrize("source,min_kernels", [("kernels.hip", 30), ("tab_copy.hip", 1), ("hbm_ceiling.hip", 4), ("win_order.hip", 3)])
 def test_kernels_compile_without_scratch(source, min_kernels):
     """Every kernel instantiation fits in registers (no scratch spills), as
     reported by hipcc's resource-usage remarks for gfx950."""

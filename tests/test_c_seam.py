@@ -64,6 +64,8 @@ def test_seam_program_put_and_probed_get():
     assert r["ref_found"] == r["n_put"] == r["ref_right"] == r["probed_found"] == 200000
     assert r["probed_fast"] > 0.9 * r["n_put"]
     assert r["fixed_found"] == 50000
+    # the same puts in the GPU's window order: every tab file equal to the batch-order store's
+    assert r["win_order_same_tab_files"] >= 256 and r["win_order_found"] == r["ref_found"]
 
 
 # ---- the C++ seam: include/shf_hash_batch_shf.hpp through the reference's SharedHashFile class ----

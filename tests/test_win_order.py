@@ -1,0 +1,198 @@
+"""Window order of a batch (shf_win_order*, csrc/win_order.hip).
+
+perm = the key indices stably sorted by win = h1 & 0xff, the window the
+reference's put/get/del take from the hash (/root/reference/src/shf.c:800,
+:893). The claim that makes the order useful is that it changes nothing: every
+structure an operation touches belongs to its key's window (lock, tab2 -> tab
+map, tabs numbered per window, shf.c:432), so a batch replayed window by
+window, batch order kept inside each window, leaves the reference's store byte
+for byte as batch order does, with the same uids. That claim is checked here
+against the reference's own put/get (oracle/_ref/libref_shf.so): on the CPU
+with the oracle's order, and on the GPU with the library's hashes and order.
+The order itself is checked bit-exact against the numpy restatement
+(Oracle.win_order: a stable argsort).
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle.oracle_py import REF_SO, Oracle, reference_put_in_order, store_files
+
+SHM = "/dev/shm" if os.path.isdir("/dev/shm") else None
+
+
+def _unique_keys(n, seed, lo=4, hi=120):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, size=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    idx = np.arange(n, dtype="<u4").view(np.uint8).reshape(n, 4)
+    starts = off[:-1].astype(np.int64)
+    for b in range(4):
+        data[starts + b] = idx[:, b]
+    return data, off
+
+
+def _same_store(data, off, hashes, perm, lockable=1):
+    """Puts the batch in batch order and in perm order into two fresh reference
+    stores; returns both results after checking the stores are identical."""
+    with tempfile.TemporaryDirectory(dir=SHM) as d:
+        a = reference_put_in_order(data, off, hashes, None, d, "batch", lockable)
+        b = reference_put_in_order(data, off, hashes, perm, d, "winord", lockable)
+        fa = store_files(d, "batch")
+        fb = {k.replace("winord", "batch"): v for k, v in store_files(d, "winord").items()}
+    n = off.size - 1
+    assert a[0] == n and b[0] == n  # every key found with its value, in either order
+    np.testing.assert_array_equal(a[1], b[1])  # the same uid for every key
+    assert sorted(fa) == sorted(fb) and len(fa) == 257  # 256 window folders' files + the store file
+    assert [k for k in fa if fa[k] != fb[k]] == []  # byte for byte
+    return a, b
+
+
+def test_oracle_order_is_a_stable_window_sort(oracle):
+    rng = np.random.default_rng(3)
+    h = rng.integers(0, 2**63, size=(5000, 2), dtype=np.int64).astype(np.uint64)
+    h[::7, 0] = (h[::7, 0] & ~np.uint64(0xFF)) | np.uint64(17)  # a crowded window
+    perm, start = Oracle.win_order(h)
+    assert sorted(perm.tolist()) == list(range(5000))
+    w = (h[perm, 0] & np.uint64(0xFF)).astype(np.int64)
+    assert (np.diff(w) >= 0).all()
+    for win in (17, int(w[0]), int(w[-1])):
+        run = perm[start[win]:start[win + 1]]
+        assert (w[start[win]:start[win + 1]] == win).all() and (np.diff(run.astype(np.int64)) > 0).all()
+    assert start[0] == 0 and start[256] == 5000
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref/libref_shf.so not built")
+@pytest.mark.parametrize("lockable", [1, 0])
+def test_window_order_leaves_the_reference_store_identical(oracle, lockable):
+    """The reference's own put/get over 60 000 keys (enough that tabs part,
+    shf.c:829-834) in batch order and in window order: identical files, uids
+    and values."""
+    data, off = _unique_keys(60000, 11)
+    h = oracle.hash_var(data, off)
+    perm, _ = Oracle.win_order(h)
+    _same_store(data, off, h, perm, lockable)
+
+
+# ---------------------------------------------------------------------------
+# GPU: the library's order against the oracle, and end to end
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def dev(hb):
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    hb.check_device()  # raises unless the current device is gfx950
+    return torch.device("cuda:0")
+
+
+def _rand_hashes(n, seed, wins=None):
+    rng = np.random.default_rng(seed)
+    h = rng.integers(0, 2**63, size=(n, 2), dtype=np.int64).astype(np.uint64)
+    if wins is not None:
+        h[:, 0] = (h[:, 0] & ~np.uint64(0xFF)) | np.asarray(wins, dtype=np.uint64)
+    return h
+
+
+def _gpu_order(hb, dev, h, **kw):
+    import torch
+
+    t = torch.from_numpy(h.view(np.int64)).to(dev)
+    perm, start = hb.win_order(t, **kw)
+    torch.cuda.synchronize(dev)
+    return perm.cpu().numpy().view(np.uint32), start.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 4095, 4096, 4097, 4 * 4096 + 1, 100_003, 1_234_567])
+def test_win_order_matches_oracle(hb, dev, n):
+    h = _rand_hashes(n, n)
+    perm, start = _gpu_order(hb, dev, h)
+    ref_perm, ref_start = Oracle.win_order(h)
+    np.testing.assert_array_equal(perm, ref_perm)
+    np.testing.assert_array_equal(start, ref_start)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["one", "two", "descending", "runs", "zero_and_255"])
+def test_win_order_skewed_windows(hb, dev, pattern):
+    """Every key in one window (every step's 64 lanes peers), two windows,
+    windows descending, long runs, only windows 0 and 255 (all eight ballots
+    agree / disagree)."""
+    n = 3 * 4096 + 77
+    i = np.arange(n)
+    wins = {"one": np.full(n, 200), "two": (i % 2) * 255, "descending": 255 - (i * 256 // n),
+            "runs": (i // 1000) % 256, "zero_and_255": np.where(i % 3 == 0, 0, 255)}[pattern]
+    h = _rand_hashes(n, 5, wins)
+    perm, start = _gpu_order(hb, dev, h)
+    ref_perm, ref_start = Oracle.win_order(h)
+    np.testing.assert_array_equal(perm, ref_perm)
+    np.testing.assert_array_equal(start, ref_start)
+
+
+@pytest.mark.gpu
+def test_win_order_of_library_hashes_side_stream_and_host(hb, dev, oracle):
+    """Hashes made by the library, the order enqueued on a side stream with a
+    caller workspace; the synchronous host-memory entry point agrees."""
+    import torch
+
+    data, off = _unique_keys(200_000, 2, 1, 300)
+    ref_h = oracle.hash_var(data, off)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(off.view(np.int64)).to(dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        h = hb.hash_var(d, o, stream=s)
+        ws = torch.empty(hb.load().shf_win_order_workspace_bytes(h.shape[0]), dtype=torch.uint8, device=dev)
+        perm, start = hb.win_order(h, workspace=ws, stream=s)
+    s.synchronize()
+    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint64), ref_h)
+    ref_perm, ref_start = Oracle.win_order(ref_h)
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), ref_perm)
+    np.testing.assert_array_equal(start.cpu().numpy().view(np.uint32), ref_start)
+    hp, hs = hb.win_order_host(ref_h)
+    np.testing.assert_array_equal(hp, ref_perm)
+    np.testing.assert_array_equal(hs, ref_start)
+    hp0, hs0 = hb.win_order_host(np.zeros((0, 2), dtype=np.uint64))
+    assert hp0.size == 0 and (hs0 == 0).all()
+
+
+@pytest.mark.gpu
+def test_win_order_rejects_bad_arguments(hb, dev):
+    import ctypes
+
+    import torch
+
+    lib = hb.load()
+    h = torch.zeros((10000, 2), dtype=torch.int64, device=dev)
+    p = torch.empty(10000, dtype=torch.int32, device=dev)
+    need = lib.shf_win_order_workspace_bytes(10000)
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    with torch.cuda.device(dev):
+        assert lib.shf_win_order_async(vp(h), 10000, vp(p), None, vp(ws), need - 1, None) == hb.ERR_ARG
+        assert lib.shf_win_order_async(vp(h), 10000, None, None, vp(ws), need, None) == hb.ERR_ARG
+        assert lib.shf_win_order_async(vp(h), 1 << 32, vp(p), None, vp(ws), need, None) == hb.ERR_ARG
+        assert lib.shf_win_order(vp(h), 10000, vp(p), None, 7) == hb.ERR_ARG
+        assert lib.shf_win_order_async(vp(h), 10000, vp(p), None, vp(ws), need, None) == hb.OK
+    torch.cuda.synchronize(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref/libref_shf.so not built")
+def test_gpu_window_order_drives_the_reference_put(hb, dev, oracle):
+    """End to end: GPU hashes and GPU window order drive the reference's own
+    put and get (60 000 keys); the store equals the batch-order store byte for
+    byte. The loops' times are printed (the order's point: the reference's get
+    finds its window in cache)."""
+    data, off = _unique_keys(60000, 12)
+    h = hb.hash_var_host(data, off)
+    np.testing.assert_array_equal(h, oracle.hash_var(data, off))
+    perm, _ = hb.win_order_host(h)
+    a, b = _same_store(data, off, h, perm)
+    print("put batch order %.0f ns/key, window order %.0f; get %.0f vs %.0f ns/key"
+          % (a[2] / 60000 * 1e9, b[2] / 60000 * 1e9, a[3] / 60000 * 1e9, b[3] / 60000 * 1e9))
