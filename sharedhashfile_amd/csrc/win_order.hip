@@ -12,22 +12,14 @@
 // the reference's get loop runs ~1.5x faster in window order.
 //
 // Three launches, all HBM-bound (16-B hash records in, 4-B indices out; the
-// records are read once: 16 + 1 + 1 + 4 B per key against 20 B at least):
-//   k_wo_hist     one wave per chunk of kWoChunk keys, four keys per lane per
-//                 step: the chunk's 256-bin histogram (LDS atomics), written
-//                 bin-major (counts[bin * chunks + chunk]), and each key's
-//                 window as one byte (wins[key]) for the scatter;
-//   k_wo_scan     one workgroup per bin: exclusive scan of the bin's chunk
-//                 counts in place, the bin's total beside them;
-//   k_wo_scatter  one wave per chunk again, in key order, 64 keys per step
-//                 (their window bytes, not the records):
-//                 the lanes of a step holding the same window find each other
-//                 with eight ballots (one per window bit), the lowest takes
-//                 the window's next positions for all of them, each lane
-//                 writes its key index at base + its rank among them. The
-//                 window's running position lives in the wave's LDS (a wave's
-//                 LDS accesses execute in order, and the compiler keeps the
-//                 order of these aliasing ones: no fence between steps).
+// records are read once: 16 + 1 + 1 + 4 B per key against 20 B at least), one
+// workgroup of four waves per chunk of kWoChunk keys:
+//   k_wo_hist     the chunk's 256-bin histogram (LDS atomics) as one row of
+//                 counts[chunk][bin], and each key's window as one byte;
+//   k_wo_scan     one workgroup per bin: exclusive scan of the bin's column of
+//                 counts over the chunks, in place; the bin's total beside;
+//   k_wo_scatter  the chunk's window bytes staged in LDS; each wave orders its
+//                 quarter, 64 keys per step (see the kernel).
 // Chunks are numbered XCD by XCD (workgroup g runs on XCD g % 8), so the runs
 // of positions that consecutive chunks write into one window's range are
 // written through the same L2 and leave HBM as whole lines.
@@ -41,9 +33,10 @@ namespace shfhb {
 
 namespace {
 
-constexpr uint32_t kWoChunk = 4096;  // keys per chunk = 64 steps of one wave
-constexpr uint32_t kWoWaves = 4;     // waves (chunks) per workgroup
-constexpr uint32_t kWoBins = 256;    // SHF_WINS_PER_SHF
+constexpr uint32_t kWoThreads = 256;                 // 4 waves
+constexpr uint32_t kWoSub = 1024;                    // keys per wave (16 steps of 64) in the scatter
+constexpr uint32_t kWoChunk = 4 * kWoSub;            // keys per workgroup (a chunk)
+constexpr uint32_t kWoBins = 256;                    // SHF_WINS_PER_SHF
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -58,49 +51,57 @@ __device__ __forceinline__ uint32_t win_of(const u32x4* hashes, uint64_t key) {
   return __builtin_nontemporal_load(&hashes[key]).x & 0xffu;  // h1's low byte (shf.c:800)
 }
 
-__global__ __launch_bounds__(64 * kWoWaves) void k_wo_hist(const u32x4* __restrict__ hashes, uint64_t n,
-                                                          uint32_t chunks, uint32_t* __restrict__ counts,
-                                                          uint32_t* __restrict__ wins) {
-  __shared__ uint32_t hist[kWoWaves][kWoBins];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t c = xcd_major(blockIdx.x, gridDim.x) * kWoWaves + wave;
-  for (uint32_t b = lane; b < kWoBins; b += 64u) hist[wave][b] = 0;
-  if (c >= chunks) return;
+// One chunk per workgroup: its 256-bin histogram (LDS atomics) as one row of
+// counts[c][*] (one coalesced 1-KiB store) and every key's window as one byte.
+// Thread t takes keys 256 s + t of step s (each load instruction reads 1 KiB of
+// consecutive records); the window bytes gather in LDS and leave as 16 B per
+// thread.
+__global__ __launch_bounds__(kWoThreads) void k_wo_hist(const u32x4* __restrict__ hashes, uint64_t n,
+                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ wins) {
+  __shared__ uint32_t hist[kWoBins];
+  __shared__ uint8_t cwb[kWoChunk];
+  const uint32_t t = threadIdx.x;
+  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
+  hist[t] = 0;
+  __syncthreads();
   const uint64_t k0 = (uint64_t)c * kWoChunk;
   const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  // step: 256 keys, lane l the four at 4 l (64 B of records, one u32 of window bytes)
-#pragma unroll 2
-  for (uint32_t i0 = 0; i0 < kn; i0 += 256u) {
-    const uint32_t i = i0 + 4u * lane;
-    uint32_t packed = 0;
+  // all sixteen record loads in flight before the first is used (past the batch:
+  // the last key's record, counted nowhere -- a load under a branch waits at once)
+  uint32_t w[16];
 #pragma unroll
-    for (uint32_t q = 0; q < 4u; ++q)
-      if (i + q < kn) {
-        const uint32_t w = win_of(hashes, k0 + i + q);
-        atomicAdd(&hist[wave][w], 1u);
-        packed |= w << (8u * q);
-      }
-    if (i < kn) wins[(k0 + i) >> 2] = packed;  // kWoChunk is a multiple of 4: k0 + i is too
+  for (uint32_t st = 0; st < 16u; ++st) w[st] = win_of(hashes, k0 + min(256u * st + t, kn - 1u));
+#pragma unroll
+  for (uint32_t st = 0; st < 16u; ++st) {
+    const uint32_t i = 256u * st + t;
+    if (i < kn) atomicAdd(&hist[w[st]], 1u);
+    cwb[i] = (uint8_t)w[st];
   }
-  for (uint32_t b = lane; b < kWoBins; b += 64u) counts[(uint64_t)b * chunks + c] = hist[wave][b];
+  __syncthreads();
+  counts[(uint64_t)c * kWoBins + t] = hist[t];
+  // 16 window bytes per thread (bytes past the batch land in the workspace's last chunk, unused)
+  reinterpret_cast<u32x4*>(wins + (k0 >> 2))[t] = reinterpret_cast<const u32x4*>(cwb)[t];
 }
 
-// Exclusive scan of one bin's chunk counts, in place; totals[bin] = the sum.
+// One workgroup per bin: exclusive scan over the chunks of counts[*][bin], in
+// place; totals[bin] = the bin's sum. Thread t takes 16 consecutive chunks per
+// round (4096 chunks = 16.7M keys a round), all 16 loads in flight at once.
+constexpr uint32_t kWoScanPer = 16;
 __global__ __launch_bounds__(256) void k_wo_scan(uint32_t* __restrict__ counts, uint32_t chunks,
                                                  uint32_t* __restrict__ totals) {
   __shared__ uint32_t wsum[4];
-  uint32_t* row = counts + (uint64_t)blockIdx.x * chunks;
-  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63u, wave = t >> 6;
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < chunks; base += 1024u) {
-    // four consecutive counts per thread
-    uint32_t v[4], s = 0;
+  for (uint32_t base = 0; base < chunks; base += 256u * kWoScanPer) {
+    uint32_t v[kWoScanPer], s = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = base + 4u * t + j;
-      v[j] = i < chunks ? row[i] : 0u;
-      s += v[j];
+    for (uint32_t j = 0; j < kWoScanPer; ++j) {
+      const uint32_t i = base + kWoScanPer * t + j;
+      const uint32_t x = counts[(uint64_t)min(i, chunks - 1u) * kWoBins + b];  // unconditional load
+      v[j] = i < chunks ? x : 0u;
     }
+#pragma unroll
+    for (uint32_t j = 0; j < kWoScanPer; ++j) s += v[j];
     uint32_t incl = s;
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -115,77 +116,150 @@ __global__ __launch_bounds__(256) void k_wo_scan(uint32_t* __restrict__ counts, 
     __syncthreads();
     uint32_t run = before + incl - s;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = base + 4u * t + j;
-      if (i < chunks) row[i] = run;
+    for (uint32_t j = 0; j < kWoScanPer; ++j) {
+      const uint32_t i = base + kWoScanPer * t + j;
+      if (i < chunks) counts[(uint64_t)i * kWoBins + b] = run;
       run += v[j];
     }
     carry += tile;
   }
-  if (t == 0) totals[blockIdx.x] = carry;
+  if (t == 0) totals[b] = carry;
 }
 
-__global__ __launch_bounds__(64 * kWoWaves) void k_wo_scatter(const uint8_t* __restrict__ wins, uint64_t n,
-                                                             uint32_t chunks, const uint32_t* __restrict__ counts,
-                                                             const uint32_t* __restrict__ totals,
-                                                             uint32_t* __restrict__ perm,
-                                                             uint32_t* __restrict__ win_start) {
-  __shared__ uint32_t next[kWoWaves][kWoBins];  // the window's next position in perm
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t c = xcd_major(blockIdx.x, gridDim.x) * kWoWaves + wave;
-  if (c >= chunks) return;
-  // bin bases: exclusive scan of the 256 totals, four consecutive bins per lane
-  uint32_t t4[4], s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    t4[j] = totals[4u * lane + j];
-    s += t4[j];
-  }
-  uint32_t incl = s;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t u = (uint32_t)__shfl_up((int)incl, d);
-    if (lane >= d) incl += u;
-  }
-  uint32_t run = incl - s;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t b = 4u * lane + j;
-    next[wave][b] = run + counts[(uint64_t)b * chunks + c];
-    if (c == 0 && win_start) win_start[b] = run;
-    run += t4[j];
-  }
-  if (c == 0 && win_start && lane == 63) win_start[kWoBins] = run;  // = n
+// One chunk per workgroup, in two phases. (1) The chunk's stable order in LDS:
+// wave v takes keys [1024 v, 1024 v + 1024) in key order, 64 per step; the
+// lanes of a step holding the same window find each other through a 64-bit LDS
+// mask per window (each sets its bit with an atomic OR -- an OR commutes, so
+// the order the LDS unit takes the lanes in does not matter -- then reads the
+// mask back), the lowest takes the window's next local positions for all of
+// them and clears the mask, and each lane puts its key at local start + its
+// rank among them. A window's first local position for wave v = the chunk's
+// keys of lower windows + the window's keys in waves 0..v-1 (histograms of the
+// chunk's window bytes). (2) The chunk's keys leave in that order, thread t
+// the positions t, t + 256, ...: a window's keys are consecutive both in LDS
+// and in perm (at the window's base, from the totals, + the chunk's prefix,
+// k_wo_scan), so each store instruction writes a few runs of whole lines
+// instead of one scattered index per lane (eight ballots per step instead of
+// the masks, with per-lane scattered stores: 47 us per 10M keys).
+// A wave's LDS accesses execute in order, and the compiler keeps the order of
+// these aliasing ones: no fence between steps.
+__global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __restrict__ wins, uint64_t n,
+                                                          uint32_t chunks, const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ totals,
+                                                          uint32_t* __restrict__ perm,
+                                                          uint32_t* __restrict__ win_start) {
+  __shared__ uint32_t next[4][kWoBins];         // per wave: the window's next local position
+  __shared__ uint32_t cw[kWoChunk / 4];         // the chunk's window bytes
+  __shared__ uint32_t sorted[kWoChunk];         // the chunk's keys in window order: offset | window << 16
+  __shared__ uint32_t gdelta[kWoBins];          // window t's perm position minus its local one
+  __shared__ uint32_t tsum[2][4];
+  __shared__ uint64_t peer_mask[4][kWoBins];    // per wave: the lanes of this step holding each window
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
+  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
   const uint64_t k0 = (uint64_t)c * kWoChunk;
   const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  uint32_t w_next = lane < kn ? wins[k0 + lane] : 0u;
-  for (uint32_t i0 = 0; i0 < kn; i0 += 64u) {
-    const uint32_t i = i0 + lane;
-    const bool valid = i < kn;
-    const uint32_t w = w_next;
-    if (i + 64u < kn) w_next = wins[k0 + i + 64u];  // the next step's window, in flight meanwhile
-    if (valid) {
-      // lanes of this step holding window w (valid lanes only: ballots see active lanes)
-      uint64_t peers = __ballot(1);  // the valid lanes
+  // every global load first: the chunk's 4 KiB of window bytes (16 B per thread;
+  // the workspace holds whole chunks), window t's total and this chunk's prefix
+  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
+  const uint32_t tot = totals[t], pre = counts[(uint64_t)c * kWoBins + t];
+  cw[4u * t + 0] = cwv.x;
+  cw[4u * t + 1] = cwv.y;
+  cw[4u * t + 2] = cwv.z;
+  cw[4u * t + 3] = cwv.w;
 #pragma unroll
-      for (uint32_t bit = 0; bit < 8u; ++bit) {
-        const bool set = (w >> bit) & 1u;
-        const uint64_t m = __ballot(set);
-        peers &= set ? m : ~m;
-      }
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-      const uint32_t base = next[wave][w];
-      perm[base + rank] = (uint32_t)(k0 + i);
-      if (rank == 0) next[wave][w] = base + (uint32_t)__popcll(peers);  // one lane per window: no conflict
+  for (int v = 0; v < 4; ++v) {
+    next[v][t] = 0;
+    peer_mask[v][t] = 0;
+  }
+  __syncthreads();
+  // each wave's histogram of its 1024 window bytes (next[] as counters for now)
+  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
+  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
+  uint32_t ws[kWoSub / 64];  // this lane's window in every step
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st)
+    if (s0 + 64u * st + lane < s1) atomicAdd(&next[wave][ws[st]], 1u);
+  __syncthreads();
+  // window t: its keys in the chunk (hc), in waves 0..v-1, and two exclusive scans over
+  // the 256 windows: of the totals (the window's base in perm) and of hc (its local start)
+  uint32_t hv[4], hc = 0;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    hv[v] = next[v][t];
+    hc += hv[v];
+  }
+  uint32_t it = tot, ih = hc;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
+    if (lane >= d) {
+      it += ut;
+      ih += uh;
     }
+  }
+  if (lane == 63) {
+    tsum[0][wave] = it;
+    tsum[1][wave] = ih;
+  }
+  __syncthreads();
+  uint32_t bbase = it - tot, lbase = ih - hc;
+  for (uint32_t v = 0; v < wave; ++v) {
+    bbase += tsum[0][v];
+    lbase += tsum[1][v];
+  }
+  if (c == 0 && win_start) {
+    win_start[t] = bbase;
+    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
+  }
+  gdelta[t] = bbase + pre - lbase;
+  {
+    uint32_t run = lbase;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      next[v][t] = run;
+      run += hv[v];
+    }
+  }
+  __syncthreads();
+  // (1) the chunk's stable window order, in LDS
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+    if (s0 + 64u * st >= s1) break;  // wave-uniform
+    const uint32_t i = s0 + 64u * st + lane;
+    const uint32_t w = ws[st];
+    const bool valid = i < s1;
+    if (valid) atomicOr(reinterpret_cast<unsigned long long*>(&peer_mask[wave][w]), 1ull << lane);
+    if (valid) {
+      const uint64_t peers = peer_mask[wave][w];
+      const uint32_t base = next[wave][w];
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+      sorted[base + rank] = i | (w << 16);
+      if (rank == 0) {  // one lane per window: no conflict
+        next[wave][w] = base + (uint32_t)__popcll(peers);
+        peer_mask[wave][w] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  // (2) out in that order: local position j holds key offset i of window w
+  uint32_t e[kWoChunk / kWoThreads];
+#pragma unroll
+  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) e[q] = sorted[min(t + kWoThreads * q, kn - 1u)];
+#pragma unroll
+  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
+    const uint32_t j = t + kWoThreads * q;
+    const uint32_t g = gdelta[e[q] >> 16] + j;
+    if (j < kn) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
   }
 }
 
 }  // namespace
 
-uint64_t win_order_workspace_bytes(uint64_t n) {  // counts, totals, then the window bytes
+uint64_t win_order_workspace_bytes(uint64_t n) {  // counts, totals, then the window bytes (whole chunks)
   const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
-  return (chunks * kWoBins + kWoBins) * sizeof(uint32_t) + ((n + 15u) & ~(uint64_t)15);
+  return (chunks * kWoBins + kWoBins) * sizeof(uint32_t) + chunks * kWoChunk;
 }
 
 hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
@@ -196,15 +270,14 @@ hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint
   }
   if (n > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit key indices
   const uint32_t chunks = (uint32_t)((n + kWoChunk - 1) / kWoChunk);
-  const uint32_t groups = (chunks + kWoWaves - 1) / kWoWaves;
   uint32_t* counts = static_cast<uint32_t*>(workspace);
   uint32_t* totals = counts + (uint64_t)chunks * kWoBins;
-  uint32_t* wins = totals + kWoBins;  // 16-B aligned: the counts are whole chunks of 256 u32
+  uint32_t* wins = totals + kWoBins;  // 16-B aligned: the counts are whole rows of 256 u32
   const u32x4* h = static_cast<const u32x4*>(hashes);
-  hipLaunchKernelGGL(k_wo_hist, dim3(groups), dim3(64 * kWoWaves), 0, st, h, n, chunks, counts, wins);
+  hipLaunchKernelGGL(k_wo_hist, dim3(chunks), dim3(kWoThreads), 0, st, h, n, counts, wins);
   hipLaunchKernelGGL(k_wo_scan, dim3(kWoBins), dim3(256), 0, st, counts, chunks, totals);
-  hipLaunchKernelGGL(k_wo_scatter, dim3(groups), dim3(64 * kWoWaves), 0, st, reinterpret_cast<const uint8_t*>(wins),
-                     n, chunks, counts, totals, perm, win_start);
+  hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, reinterpret_cast<const uint8_t*>(wins), n,
+                     chunks, counts, totals, perm, win_start);
   return hipGetLastError();
 }
 
