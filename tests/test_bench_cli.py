@@ -105,6 +105,7 @@ def test_grid_threads_match_the_launchers():
     assert bench.grid_threads("var", 100_000_000) == 781_250 * 128  # 1 562 500 tiles, two per workgroup
     assert bench.grid_threads("var", 65) == 128
     assert bench.grid_threads("tabpart", 1024) == 1024 * 512
+    assert bench.grid_threads("winorder", 10_000_000) == 2442 * 256  # one 256-thread workgroup per 4096 keys
     assert bench.grid_threads("ceil_read16", 64) == 256
     assert bench.grid_threads("ceil_read16w1", 128) == 128
     assert bench.grid_threads("ceil_copynt", 10_000_000) == 10_000_128
