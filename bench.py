@@ -78,7 +78,10 @@ KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
                "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
                "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128<true>",
-               "winorder": "k_wo_scatter"}
+               "winorder": "k_wo_"}
+# workloads whose one call is several kernels: their counters are summed over the kernels
+# (each kernel's median per launch), so traffic covers the whole call
+MULTI_KERNEL = {"winorder": ["k_wo_hist", "k_wo_scan", "k_wo_scatter"]}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart", "winorder"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
                   "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
@@ -314,7 +317,7 @@ def grid_threads(name, n):
     if name == "tabpart":
         return n * 512                  # k_tab_split: one 512-thread workgroup per tab
     if name == "winorder":
-        return ((n + 4095) // 4096 + 3) // 4 * 256  # k_wo_scatter: 4 waves per workgroup, a 4096-key chunk each
+        return (n + 4095) // 4096 * 256  # k_wo_scatter: one 256-thread workgroup per 4096-key chunk
     return None
 
 
@@ -981,9 +984,26 @@ def parse_pmc_rows(rows, grids):
         except ValueError:
             grid = -1
         for w, g in grids.items():
-            if KERNEL_SYMS[w] in name and (g is None or grid < 0 or grid == g):
+            if w in MULTI_KERNEL:
+                for sym in MULTI_KERNEL[w]:
+                    if sym in name:
+                        vals.setdefault(w, {}).setdefault((sym, row.get("Counter_Name")), []).append(
+                            float(row["Counter_Value"]))
+            elif KERNEL_SYMS[w] in name and (g is None or grid < 0 or grid == g):
                 vals.setdefault(w, {}).setdefault(row.get("Counter_Name"), []).append(float(row["Counter_Value"]))
     return vals
+
+
+def pmc_medians(cs):
+    """{counter: median per launch} of one workload's rows; a multi-kernel
+    workload's counters are the sum of its kernels' medians."""
+    out = {}
+    for c, v in cs.items():
+        if isinstance(c, tuple):
+            out[c[1]] = out.get(c[1], 0.0) + float(np.median(v))
+        else:
+            out[c] = float(np.median(v))
+    return out
 
 
 def collect_pmc(args, names):
@@ -1021,8 +1041,7 @@ def collect_pmc(args, names):
                 rows += list(csv.DictReader(fh))
         shutil.rmtree(outdir, ignore_errors=True)
         for w, cs in parse_pmc_rows(rows, grids).items():
-            for c, v in cs.items():
-                res[w][c] = float(np.median(v))
+            res[w].update(pmc_medians(cs))
     return res, ("per launch, median over the child's launches of each workload's kernel at its own grid size; "
                  "configs 2/3 at <= 10M keys. traffic = the bytes the L2s read from the fabric, from the 32/64/128-B "
                  "read request counts (TCC_EA0_RDREQ_*B_sum; Infinity-Cache hits included), + WRITE_SIZE; "

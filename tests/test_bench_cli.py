@@ -173,3 +173,17 @@ def test_line_for_eight_ranks_carries_per_rank_fields():
     assert line["verified"] is True and line["secondary"]["ceil_copy"]["unit"] == "lanes/s"
     json_line = bench.json.dumps(line)
     assert "all_visible_cpus_extrapolated" not in json_line and "HBM_COPY" not in json_line
+
+
+def test_multi_kernel_workload_counters_sum_over_its_kernels():
+    rows = []
+    for k, grid, fetch in (("k_wo_hist", 625152, 100.0), ("k_wo_scan", 65536, 10.0), ("k_wo_scatter", 625152, 5.0)):
+        for rep in range(3):
+            rows.append({"Kernel_Name": "void shfhb::(anonymous namespace)::%s(...)" % k, "Grid_Size": str(grid),
+                         "Counter_Name": "FETCH_SIZE", "Counter_Value": str(fetch + rep)})
+    rows.append({"Kernel_Name": "void shfhb::k_fixed16<0>(...)", "Grid_Size": "256", "Counter_Name": "FETCH_SIZE",
+                 "Counter_Value": "7"})
+    vals = bench.parse_pmc_rows(rows, {"winorder": bench.grid_threads("winorder", 10_000_000), "fixed16": 256})
+    m = bench.pmc_medians(vals["winorder"])
+    assert m["FETCH_SIZE"] == 101.0 + 11.0 + 6.0  # the three kernels' medians, summed
+    assert bench.pmc_medians(vals["fixed16"]) == {"FETCH_SIZE": 7.0}
