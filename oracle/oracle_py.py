@@ -152,6 +152,9 @@ def reference_lib():
     lib.ref_put_in_order.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, vp, vp, vp, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     lib.ref_put_in_order.restype = ctypes.c_int64
+    lib.ref_put_get_procs.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    lib.ref_put_get_procs.restype = ctypes.c_int64
     lib.ref_part_capture.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, u64, u32, u32, u32, u32,
                                      ctypes.c_char_p]
     lib.ref_part_capture.restype = ctypes.c_int64
@@ -252,3 +255,26 @@ def store_files(folder, name):
             with open(p, "rb") as fh:
                 out[os.path.relpath(p, root)] = fh.read()
     return out
+
+
+def reference_put_get_procs(data, offsets, hashes, order, starts, folder, name, lockable=1):
+    """The reference's put then get loops on len(starts) - 1 forked processes,
+    process t over keys order[starts[t] .. starts[t+1]) (order None = batch
+    order), each with its own handle on store folder/name (oracle/ref_export.c
+    ref_put_get_procs). Call it from a process that has not touched the GPU.
+    Returns (found, put_seconds, get_seconds)."""
+    lib = reference_lib()
+    if lib is None:
+        raise RuntimeError("oracle/_ref/libref_shf.so not built")
+    data = np.ascontiguousarray(data).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    hashes = np.ascontiguousarray(hashes, dtype=np.uint64)
+    starts = np.ascontiguousarray(starts, dtype=np.uint64)
+    order = None if order is None else np.ascontiguousarray(order, dtype=np.uint32)
+    ps, gs = ctypes.c_double(), ctypes.c_double()
+    found = lib.ref_put_get_procs(folder.encode(), name.encode(), data.ctypes.data, offsets.ctypes.data,
+                                    hashes.ctypes.data, order.ctypes.data if order is not None else None,
+                                    starts.ctypes.data, starts.size - 1, lockable, ctypes.byref(ps), ctypes.byref(gs))
+    if found < 0:
+        raise RuntimeError("ref_put_get_procs failed (%d)" % found)
+    return found, ps.value, gs.value

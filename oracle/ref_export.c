@@ -29,6 +29,7 @@
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <sys/types.h>
+#include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -339,4 +340,83 @@ int64_t ref_put_in_order(const char *folder, const char *name, const uint8_t *by
     if (get_seconds) *get_seconds = t2 - t1;
     shf_detach(shf);
     return good;
+}
+
+/* ---- window order with processes: the reference's put/get loops on T processes --
+ * (The reference's lock is a process-level lock: several handles in one
+ * process are not a supported use, so the workers are forked processes, as in
+ * the reference's own multi-process tests.) Worker t attaches its own handle
+ * to store folder/name (created here first) and runs keys idx[starts[t] ..
+ * starts[t+1]) (idx NULL: batch order) through shf_put_key_val (value: the key
+ * index); after every worker's puts, the same keys through
+ * shf_get_key_val_copy, checking each value. With idx = the window order and
+ * starts at window boundaries (shf_win_order's win_start), the workers'
+ * windows are disjoint: no window lock or window structure is shared. The
+ * caller must not have started threads the children need (call it from a
+ * process that has not touched the GPU). Returns the keys found with their
+ * value, or < 0. */
+static int64_t ref_worker(const char *folder, const char *name, const uint8_t *bytes, const uint64_t *offsets,
+                          const uint64_t *hashes, const uint32_t *idx, uint64_t lo, uint64_t hi, int lockable, int op)
+{
+    SHF *shf = shf_attach(folder, name, 0);
+    if (!shf) return -1;
+    shf_set_is_lockable(shf, (uint32_t)lockable);
+    int64_t good = 0;
+    for (uint64_t j = lo; j < hi; ++j) {
+        const uint64_t i = idx ? idx[j] : j;
+        shf_hash.u64[0] = hashes[2 * i];
+        shf_hash.u64[1] = hashes[2 * i + 1];
+        shf_hash_key = (const char *)bytes + offsets[i];
+        shf_hash_key_len = (uint32_t)(offsets[i + 1] - offsets[i]);
+        if (op == 0) good += shf_put_key_val(shf, (const char *)&i, sizeof(i)) == SHF_RET_KEY_PUT;
+        else good += shf_get_key_val_copy(shf) == SHF_RET_KEY_FOUND && ref_val_is(i);
+    }
+    shf_detach(shf);
+    return good;
+}
+
+int64_t ref_put_get_procs(const char *folder, const char *name, const uint8_t *bytes, const uint64_t *offsets,
+                          const uint64_t *hashes, const uint32_t *idx, const uint64_t *starts, int nprocs,
+                          int lockable, double *put_seconds, double *get_seconds)
+{
+    if (nprocs < 1 || nprocs > 256) return -1;
+    shf_init();
+    SHF *shf = shf_attach(folder, name, 0);
+    if (!shf) return -1;
+    int64_t *res = mmap(NULL, 256 * sizeof(int64_t), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    if (res == MAP_FAILED) return -2;
+    int64_t found = 0;
+    for (int op = 0; op < 2; ++op) {
+        const double t0 = ref_now();
+        pid_t pids[256];
+        for (int t = 0; t < nprocs; ++t) {
+            pids[t] = fork();
+            if (pids[t] == 0) {
+                res[t] = ref_worker(folder, name, bytes, offsets, hashes, idx, starts[t], starts[t + 1], lockable, op);
+                _exit(0);
+            }
+            if (pids[t] < 0) return -2;
+        }
+        int64_t good = 0;
+        for (int t = 0; t < nprocs; ++t) {
+            int st = 0;
+            waitpid(pids[t], &st, 0);
+            good += res[t];
+        }
+        const double dt = ref_now() - t0;
+        if (op == 0) {
+            if (put_seconds) *put_seconds = dt;
+            if (good != (int64_t)(starts[nprocs] - starts[0])) {
+                munmap(res, 256 * sizeof(int64_t));
+                shf_detach(shf);
+                return -3;
+            }
+        } else {
+            if (get_seconds) *get_seconds = dt;
+            found = good;
+        }
+    }
+    munmap(res, 256 * sizeof(int64_t));
+    shf_detach(shf);
+    return found;
 }

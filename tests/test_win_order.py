@@ -196,3 +196,23 @@ def test_gpu_window_order_drives_the_reference_put(hb, dev, oracle):
     a, b = _same_store(data, off, h, perm)
     print("put batch order %.0f ns/key, window order %.0f; get %.0f vs %.0f ns/key"
           % (a[2] / 60000 * 1e9, b[2] / 60000 * 1e9, a[3] / 60000 * 1e9, b[3] / 60000 * 1e9))
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref/libref_shf.so not built")
+def test_window_disjoint_workers_put_and_find_every_key(oracle):
+    """What win_start is for: 4 forked worker processes of the reference (each
+    its own handle, the reference's multi-process use) take whole windows of
+    the window order, and every key is put and found with its value; the same
+    with batch-order ranges. (CPU only: the workers are forked, and a -m gpu
+    run's process has touched the GPU.)"""
+    from oracle.oracle_py import reference_put_get_procs
+
+    data, off = _unique_keys(80000, 21)
+    h = oracle.hash_var(data, off)
+    perm, start = Oracle.win_order(h)
+    n = off.size - 1
+    for order, starts in ((None, [0, n // 4, n // 2, 3 * n // 4, n]),
+                          (perm, [start[0], start[64], start[128], start[192], start[256]])):
+        with tempfile.TemporaryDirectory(dir=SHM) as d:
+            found, _, _ = reference_put_get_procs(data, off, h, order, np.array(starts, np.uint64), d, "w", 1)
+        assert found == n
