@@ -217,12 +217,35 @@ int main(int argc, char **argv)
     const uint64_t wfound2 = shf_get_batch_win_ordered(wshf, bytes, off, n, h, permq, check_value, NULL);
     if (wfound2 != ref_found || good_values != ref_right) return fail("window-ordered get: answers differ");
 
+    /* 6. window ranges: 4 workers, each its own handle on a third store, each putting windows
+     *    [64 w, 64 w + 64) of the same order (one after another here: this process has touched the
+     *    GPU, so it forks nothing; tools/win_order_procs.py times the ranges on forked workers) */
+    uint32_t *ws = malloc(257 * sizeof *ws);
+    if (shf_win_order(h, n_put, perm, ws, SHF_HASH_MEM_HOST) != SHF_HB_OK) return fail("shf_win_order ranges");
+    int64_t range_put = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+        SHF *mine = shf_attach(folder, "seamrange", 0);
+        if (!mine) return fail("shf_attach ranges");
+        range_put += shf_put_batch_win_range(mine, bytes, off, h, perm, ws, 64 * w, 64 * w + 64, vals, voff);
+        shf_detach(mine);
+    }
+    if (shf_put_batch_win_range(shf, bytes, off, h, perm, ws, 3, 2, vals, voff) != SHF_HB_ERR_ARG)
+        return fail("window ranges: bad range accepted");
+    SHF *rshf = shf_attach(folder, "seamrange", 0);
+    if (!rshf) return fail("shf_attach ranges");
+    if (range_put != (int64_t)n_put) return fail("window ranges: puts");
+    good_values = 0;
+    const uint64_t rfound = shf_get_batch_win_ordered(rshf, bytes, off, n, h, permq, check_value, NULL);
+    if (rfound != ref_found || good_values != ref_right) return fail("window ranges: get answers differ");
+    shf_detach(rshf);
+
     printf("{\"n_put\": %llu, \"n_query\": %llu, \"ref_found\": %llu, \"ref_right\": %llu, \"probed_found\": %llu, "
            "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu, \"win_order_same_tab_files\": %llu, "
-           "\"win_order_found\": %llu}\n",
+           "\"win_order_found\": %llu, \"win_range_put\": %lld}\n",
            (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
            (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
-           (unsigned long long)ffound, (unsigned long long)same_files, (unsigned long long)wfound2);
+           (unsigned long long)ffound, (unsigned long long)same_files, (unsigned long long)wfound2,
+           (long long)range_put);
     shf_detach(wshf);
     /* the stores' files go with the folder (shf_del would run `du` and `rm` through popen) */
     shf_detach(shf);

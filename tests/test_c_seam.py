@@ -66,6 +66,7 @@ def test_seam_program_put_and_probed_get():
     assert r["fixed_found"] == 50000
     # the same puts in the GPU's window order: every tab file equal to the batch-order store's
     assert r["win_order_same_tab_files"] >= 256 and r["win_order_found"] == r["ref_found"]
+    assert r["win_range_put"] == r["n_put"]  # four window ranges, one handle each, put every key
 
 
 # ---- the C++ seam: include/shf_hash_batch_shf.hpp through the reference's SharedHashFile class ----
