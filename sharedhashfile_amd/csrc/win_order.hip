@@ -11,13 +11,13 @@
 // consecutive operations then find the window's lock, map and tabs in cache:
 // the reference's get loop runs ~1.5x faster in window order.
 //
-// Three launches, all HBM-bound (16-B hash records in, 4-B indices out; the
+// Four launches, HBM-bound (16-B hash records in, 4-B indices out; the
 // records are read once: 16 + 1 + 1 + 4 B per key against 20 B at least), one
 // workgroup of four waves per chunk of kWoChunk keys:
 //   k_wo_hist     the chunk's 256-bin histogram (LDS atomics) as one row of
 //                 counts[chunk][bin], and each key's window as one byte;
-//   k_wo_scan     one workgroup per bin: exclusive scan of the bin's column of
-//                 counts over the chunks, in place; the bin's total beside;
+//   k_wo_scan_*   the chunks' counts scanned per bin in two levels (blocks of
+//                 64 rows, then the blocks' sums), rows read whole;
 //   k_wo_scatter  the chunk's window bytes staged in LDS; each wave orders its
 //                 quarter, 64 keys per step (see the kernel).
 // Chunks are numbered XCD by XCD (workgroup g runs on XCD g % 8), so the runs
@@ -83,47 +83,49 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_hist(const u32x4* __restrict_
   reinterpret_cast<u32x4*>(wins + (k0 >> 2))[t] = reinterpret_cast<const u32x4*>(cwb)[t];
 }
 
-// One workgroup per bin: exclusive scan over the chunks of counts[*][bin], in
-// place; totals[bin] = the bin's sum. Thread t takes 16 consecutive chunks per
-// round (4096 chunks = 16.7M keys a round), all 16 loads in flight at once.
-constexpr uint32_t kWoScanPer = 16;
-__global__ __launch_bounds__(256) void k_wo_scan(uint32_t* __restrict__ counts, uint32_t chunks,
-                                                 uint32_t* __restrict__ totals) {
-  __shared__ uint32_t wsum[4];
-  const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < chunks; base += 256u * kWoScanPer) {
-    uint32_t v[kWoScanPer], s = 0;
+// The chunks' counts scanned per bin in two levels, rows read whole (a row =
+// one chunk's 256 counts, 1 KiB; thread t = bin t):
+//   k_wo_scan_blocks  one workgroup per block of kWoScanBlock chunks: exclusive
+//                     prefix of each bin over the block's rows, in place, and
+//                     the block's sums (bsum[block][bin]);
+//   k_wo_scan_top     one workgroup: exclusive prefix of each bin over the
+//                     blocks' sums, in place, and the bins' totals.
+// A chunk's prefix is then counts[c][bin] + bsum[c / kWoScanBlock][bin].
+// (One workgroup per bin reading its column, 4-B words 1 KiB apart: 13.4 us
+// per 10M keys.)
+constexpr uint32_t kWoScanBlock = 64;
+__global__ __launch_bounds__(256) void k_wo_scan_blocks(uint32_t* __restrict__ counts, uint32_t chunks,
+                                                        uint32_t* __restrict__ bsum) {
+  const uint32_t t = threadIdx.x, c0 = blockIdx.x * kWoScanBlock;
+  uint32_t v[kWoScanBlock];
 #pragma unroll
-    for (uint32_t j = 0; j < kWoScanPer; ++j) {
-      const uint32_t i = base + kWoScanPer * t + j;
-      const uint32_t x = counts[(uint64_t)min(i, chunks - 1u) * kWoBins + b];  // unconditional load
-      v[j] = i < chunks ? x : 0u;
-    }
+  for (uint32_t r = 0; r < kWoScanBlock; ++r)  // every load in flight first (past the end: the last row, unused)
+    v[r] = counts[(uint64_t)min(c0 + r, chunks - 1u) * kWoBins + t];
+  uint32_t run = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < kWoScanPer; ++j) s += v[j];
-    uint32_t incl = s;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)incl, d);
-      if (lane >= d) incl += u;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t before = carry;
-    for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
-    const uint32_t tile = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
-    uint32_t run = before + incl - s;
-#pragma unroll
-    for (uint32_t j = 0; j < kWoScanPer; ++j) {
-      const uint32_t i = base + kWoScanPer * t + j;
-      if (i < chunks) counts[(uint64_t)i * kWoBins + b] = run;
-      run += v[j];
-    }
-    carry += tile;
+  for (uint32_t r = 0; r < kWoScanBlock; ++r) {
+    if (c0 + r < chunks) counts[(uint64_t)(c0 + r) * kWoBins + t] = run;
+    run += c0 + r < chunks ? v[r] : 0u;
   }
-  if (t == 0) totals[b] = carry;
+  bsum[(uint64_t)blockIdx.x * kWoBins + t] = run;
+}
+
+__global__ __launch_bounds__(256) void k_wo_scan_top(uint32_t* __restrict__ bsum, uint32_t blocks,
+                                                     uint32_t* __restrict__ totals) {
+  constexpr uint32_t kBatch = 16;
+  const uint32_t t = threadIdx.x;
+  uint32_t run = 0;
+  for (uint32_t b0 = 0; b0 < blocks; b0 += kBatch) {
+    uint32_t v[kBatch];
+#pragma unroll
+    for (uint32_t r = 0; r < kBatch; ++r) v[r] = bsum[(uint64_t)min(b0 + r, blocks - 1u) * kWoBins + t];
+#pragma unroll
+    for (uint32_t r = 0; r < kBatch; ++r) {
+      if (b0 + r < blocks) bsum[(uint64_t)(b0 + r) * kWoBins + t] = run;
+      run += b0 + r < blocks ? v[r] : 0u;
+    }
+  }
+  totals[t] = run;
 }
 
 // One chunk per workgroup, in two phases. (1) The chunk's stable order in LDS:
@@ -138,13 +140,14 @@ __global__ __launch_bounds__(256) void k_wo_scan(uint32_t* __restrict__ counts, 
 // chunk's window bytes). (2) The chunk's keys leave in that order, thread t
 // the positions t, t + 256, ...: a window's keys are consecutive both in LDS
 // and in perm (at the window's base, from the totals, + the chunk's prefix,
-// k_wo_scan), so each store instruction writes a few runs of whole lines
+// k_wo_scan_*), so each store instruction writes a few runs of whole lines
 // instead of one scattered index per lane (eight ballots per step instead of
 // the masks, with per-lane scattered stores: 47 us per 10M keys).
 // A wave's LDS accesses execute in order, and the compiler keeps the order of
 // these aliasing ones: no fence between steps.
 __global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __restrict__ wins, uint64_t n,
                                                           uint32_t chunks, const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ bsum,
                                                           const uint32_t* __restrict__ totals,
                                                           uint32_t* __restrict__ perm,
                                                           uint32_t* __restrict__ win_start) {
@@ -161,7 +164,8 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __rest
   // every global load first: the chunk's 4 KiB of window bytes (16 B per thread;
   // the workspace holds whole chunks), window t's total and this chunk's prefix
   const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
-  const uint32_t tot = totals[t], pre = counts[(uint64_t)c * kWoBins + t];
+  const uint32_t tot = totals[t];
+  const uint32_t pre = counts[(uint64_t)c * kWoBins + t] + bsum[(uint64_t)(c / kWoScanBlock) * kWoBins + t];
   cw[4u * t + 0] = cwv.x;
   cw[4u * t + 1] = cwv.y;
   cw[4u * t + 2] = cwv.z;
@@ -259,7 +263,8 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __rest
 
 uint64_t win_order_workspace_bytes(uint64_t n) {  // counts, totals, then the window bytes (whole chunks)
   const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
-  return (chunks * kWoBins + kWoBins) * sizeof(uint32_t) + chunks * kWoChunk;
+  const uint64_t blocks = (chunks + kWoScanBlock - 1) / kWoScanBlock;
+  return ((chunks + blocks) * kWoBins + kWoBins) * sizeof(uint32_t) + chunks * kWoChunk;
 }
 
 hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
@@ -270,14 +275,17 @@ hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint
   }
   if (n > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit key indices
   const uint32_t chunks = (uint32_t)((n + kWoChunk - 1) / kWoChunk);
+  const uint32_t blocks = (chunks + kWoScanBlock - 1) / kWoScanBlock;
   uint32_t* counts = static_cast<uint32_t*>(workspace);
-  uint32_t* totals = counts + (uint64_t)chunks * kWoBins;
-  uint32_t* wins = totals + kWoBins;  // 16-B aligned: the counts are whole rows of 256 u32
+  uint32_t* bsum = counts + (uint64_t)chunks * kWoBins;
+  uint32_t* totals = bsum + (uint64_t)blocks * kWoBins;
+  uint32_t* wins = totals + kWoBins;  // 16-B aligned: whole rows of 256 u32 before it
   const u32x4* h = static_cast<const u32x4*>(hashes);
   hipLaunchKernelGGL(k_wo_hist, dim3(chunks), dim3(kWoThreads), 0, st, h, n, counts, wins);
-  hipLaunchKernelGGL(k_wo_scan, dim3(kWoBins), dim3(256), 0, st, counts, chunks, totals);
+  hipLaunchKernelGGL(k_wo_scan_blocks, dim3(blocks), dim3(256), 0, st, counts, chunks, bsum);
+  hipLaunchKernelGGL(k_wo_scan_top, dim3(1), dim3(256), 0, st, bsum, blocks, totals);
   hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, reinterpret_cast<const uint8_t*>(wins), n,
-                     chunks, counts, totals, perm, win_start);
+                     chunks, counts, bsum, totals, perm, win_start);
   return hipGetLastError();
 }
 
