@@ -108,7 +108,8 @@ def _gpu_order(hb, dev, h, **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 4095, 4096, 4097, 4 * 4096 + 1, 100_003, 1_234_567])
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 4095, 4096, 4097, 4 * 4096 + 1, 64 * 4096, 64 * 4096 + 1, 100_003,
+                               1_234_567, 10_000_003])
 def test_win_order_matches_oracle(hb, dev, n):
     h = _rand_hashes(n, n)
     perm, start = _gpu_order(hb, dev, h)
