@@ -1,12 +1,12 @@
 #!/bin/bash
-# window order: tree build against the first version (tools/_ab/lib_wo5.so), bench line each, then rocprof of the tree
+# window order: tree build against the first version (tools/_ab/lib_wo7.so), bench line each, then rocprof of the tree
 set -e
 o=gpurun_out/wo3; mkdir -p $o
 export TMPDIR=/tmp
 timeout -k 10 200 python bench.py --only winorder --no-cpu --no-host-inclusive --traffic off > $o/tree.json 2> $o/tree.err
 grep "\[bench\]" $o/tree.err
 cp sharedhashfile_amd/libshf_hash_batch.so $o/tree.so
-cp tools/_ab/lib_wo5.so sharedhashfile_amd/libshf_hash_batch.so
+cp tools/_ab/lib_wo7.so sharedhashfile_amd/libshf_hash_batch.so
 timeout -k 10 200 python bench.py --only winorder --no-cpu --no-host-inclusive --traffic off > $o/prev.json 2> $o/prev.err || true
 grep "\[bench\]" $o/prev.err || true
 cp $o/tree.so sharedhashfile_amd/libshf_hash_batch.so
