@@ -71,20 +71,22 @@ BOX_CPU_SHARE = 16   # host threads per GPU on the GPU box (its sizing rule for 
 # rocprofv3 kernel-name substrings of each workload's kernel (PMC passes; rows
 # are also matched on the launch's grid size, Workload.grid)
 KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1b": "k_fixed16<0>",
-               "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>",
+               "fixed256": "k_tiled<0, 8>", "var": "k_span_pp<0", "probe16": "k_fixed16<2>", "probe16_hbm": "k_fixed16<2>",
                "tabpart": "k_tab_split", "ceil_copy": "k_ceil_copy(", "ceil_copy_hot": "k_ceil_copy(",
                "ceil_copy_1b": "k_ceil_copy(", "ceil_read16": "k_ceil_read16<false", "ceil_read16nt": "k_ceil_read16<true, 256",
                "ceil_read16w1": "k_ceil_read16<true, 64", "ceil_gather128": "k_ceil_gather128<false>",
                "ceil_stream16u": "k_ceil_stream16u", "ceil_valu_add": "k_ceil_valu<0>",
                "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
                "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128<true>",
+               "ceil_probe_rows_hbm": "k_ceil_gather128<true>",
                "winorder": "k_wo_"}
 # workloads whose one call is several kernels: their counters are summed over the kernels
 # (each kernel's median per launch), so traffic covers the whole call
 MULTI_KERNEL = {"winorder": ["k_wo_hist", "k_wo_scan", "k_wo_scatter"]}
-HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "tabpart", "winorder"]
+HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "probe16_hbm", "tabpart",
+                  "winorder"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
-                  "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
+                  "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_probe_rows_hbm", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
                   "ceil_valu_mul"]
 # the ceiling each hashing line is reported against: the best copy of the same bytes on the same buffers
 # (one lane per 16 B as k_fixed16 moves them, plain or nontemporal stores), measured in this run right after
@@ -92,15 +94,17 @@ CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot"
 CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copynt"], "fixed16_hot": ["ceil_copy_hot", "ceil_copynt_hot"],
               "shard1b": ["ceil_copy_1b", "ceil_copynt_1b"], "fixed256": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
               "var": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
-              "probe16": ["ceil_probe_rows"], "tabpart": ["ceil_copy", "ceil_copynt"],
+              "probe16": ["ceil_probe_rows"], "probe16_hbm": ["ceil_probe_rows_hbm"], "tabpart": ["ceil_copy", "ceil_copynt"],
               "winorder": ["ceil_copy", "ceil_copynt"]}
 # timing order: each ceiling right after the line it bounds (same buffers, same thermal state)
 ORDER = ["fixed16", "ceil_copy", "ceil_copynt", "fixed16_hot", "ceil_copy_hot", "ceil_copynt_hot", "shard1b",
          "ceil_copy_1b", "ceil_copynt_1b", "fixed256", "ceil_read16", "ceil_read16nt", "ceil_read16w1", "var", "probe16", "ceil_probe_rows",
+         "probe16_hbm", "ceil_probe_rows_hbm",
          "ceil_gather128", "tabpart", "ceil_stream16u", "winorder", "ceil_valu_add", "ceil_valu_mul"]
 # the pattern whose known byte count calibrates each line's FETCH_SIZE
 FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
                 "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
+                "probe16_hbm": "ceil_gather128",
                 "tabpart": "ceil_stream16u", "winorder": "ceil_copy"}
 # bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
 CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copynt": 16, "ceil_read16": 256, "ceil_read16nt": 256, "ceil_read16w1": 256,
@@ -124,7 +128,10 @@ def parse(argv=None):
     p.add_argument("--keysvar", type=int, default=100_000_000, help="configs[3]: 8..512-B keys per GPU")
     p.add_argument("--only", default="", help="comma list of %s, %s" % (",".join(HASH_WORKLOADS),
                                                                            ",".join(CEIL_WORKLOADS)))
-    p.add_argument("--probe-tabs", type=int, default=16, help="probe16: physical tabs per window in the index")
+    p.add_argument("--probe-tabs", type=int, default=16,
+                   help="probe16: physical tabs per window in the index (16: 256 MiB of rows, cache-resident)")
+    p.add_argument("--probe-tabs-hbm", type=int, default=128,
+                   help="probe16_hbm: tabs per window (128: 2 GiB of rows, well past the 256 MiB Infinity Cache)")
     p.add_argument("--tab-jobs", type=int, default=1024, help="tabpart: tabs parted per step (f4)")
     p.add_argument("--var-kernel", default="auto", choices=["auto", "span", "span_pp", "generic", "round"])
     p.add_argument("--fixed-kernel", default="auto", choices=["auto", "fixed16", "tiled", "generic", "span"])
@@ -144,6 +151,8 @@ def parse(argv=None):
     p.add_argument("--warmup-min-s", type=float, default=WARMUP_MIN_S,
                    help="keep warming up (untimed) until this many seconds of the workload have run")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--detail-out", default=None,
+                   help="file for the full record (PMC, calibration, per-rank); default gpurun_out/bench_detail_nN.json")
     return p.parse_args(argv)
 
 
@@ -308,7 +317,7 @@ def grid_threads(name, n):
     rocprofv3's Grid_Size of that launch (the PMC rows are matched on it)."""
     if name == "ceil_read16w1":
         return n                        # one 64-thread workgroup per 64 lanes (n a multiple of 64)
-    if name in ("fixed16", "fixed16_hot", "shard1b", "probe16") or name.startswith("ceil_"):
+    if name in ("fixed16", "fixed16_hot", "shard1b", "probe16", "probe16_hbm") or name.startswith("ceil_"):
         return _up(n, 256)              # 256-thread blocks, one key / lane per thread
     if name == "fixed256":
         return _up(n, 64)               # k_tiled: one 64-thread workgroup per 64-key tile
@@ -333,7 +342,9 @@ def ceil_launcher(hb, kind, src, src_bytes, idx, dst, n, dev):
 
     import torch
 
-    fn = hb.load().shf_hb_ceiling_async
+    from sharedhashfile_amd import bench_ceiling
+
+    fn = bench_ceiling.load().shf_hb_ceiling_async
     argv = (ctypes.c_int(kind), ctypes.c_void_p(src), ctypes.c_uint64(src_bytes), ctypes.c_void_p(idx or 0),
             ctypes.c_void_p(dst), ctypes.c_uint64(n), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
 
@@ -427,46 +438,10 @@ def make_workloads(args, dev, rank, world=1):
                            "%d variable keys U[8,512] B, %.3f GB of key bytes" % (n, total / 1e9),
                            lambda d=data, o=off, out=out: verify_var(d, o, out, VERIFY_SAMPLES, 15),
                            grid_threads("var", n) if args.var_kernel in ("auto", "span_pp") else None))
-    if "probe16" in only:
-        # Row pre-probe: hash + row scan of every key against an index holding
-        # all of them (a get-hit batch). Bytes per key: 16 key + 128 row +
-        # 16 record; the 2 MiB tab map is read once per launch.
-        from sharedhashfile_amd.rowindex import synthetic_index
-
-        n = args.keys16
-        keys = device_random_bytes(n * 16, seed_base + 5, dev)
-        h = hb.hash_fixed(keys, 16)
-        tab_slot, rows, n_slots, placed = synthetic_index(h, tabs_per_win=args.probe_tabs)
-        index = hb.RowIndex(n_slots, tab_slot, rows)
-        host_index = (tab_slot.cpu().numpy().view(np.uint32), rows.cpu().numpy(), n_slots)
-        # each key's row (slot * 512 + row) in key order: the probe's own row sequence, for its ceiling
-        h1 = h[:, 0]
-        T = args.probe_tabs
-        rid = (((h1 & 0xFF) * T + ((h1 >> 16) & 0x7FF) % T) * 512 + ((h1 >> 32) & 0x1FF)).to(torch.int32)
-        bufs["probe_rows"] = (rows, rid, n)
-        del h, tab_slot, h1
-        out = torch.empty((n, 4), dtype=torch.int32, device=dev)
-
-        def verify_probe(keys=keys, out=out, hx=host_index):
-            import torch as _t
-
-            from oracle.oracle_py import Oracle
-
-            o = Oracle()
-            idx = _sample_idx(n, VERIFY_SAMPLES, 16)
-            ti = _t.from_numpy(idx).to(dev)
-            k = keys.view(n, 16).index_select(0, ti).cpu().numpy()
-            want = o.probe(o.hash_fixed(k, 16), hx[0], hx[1], hx[2])
-            got = out.index_select(0, ti).cpu().numpy().view(np.uint32)
-            return bool(np.array_equal(got, want)), int(idx.size)
-
-        w = Workload("probe16", n, 16 + 128 + 16 + 4 * 256 * 2048 / n,
-                     [lambda k=keys, o=out, ix=index: hb.probe_fixed(ix, k, 16, out=o)],
-                     "k_fixed16<kOutProbe>", "%d fixed 16-B keys hashed and probed against a row index of "
-                     "%d slots (%.0f MiB) holding %d of them" % (n, n_slots, n_slots / 16, placed), verify_probe,
-                     grid_threads("probe16", n))
-        w.index = index
-        wl.append(w)
+    for pname, tabs, dn in (("probe16", args.probe_tabs, 0), ("probe16_hbm", args.probe_tabs_hbm, 256)):
+        if pname in only:
+            wl.append(probe_workload(args, dev, pname, tabs, args.keys16 - dn, seed_base + (5 if dn == 0 else 8),
+                                     bufs))
     if "tabpart" in only:
         wl.append(tab_workload(args, dev, seed_base))
     if "winorder" in only:
@@ -476,6 +451,59 @@ def make_workloads(args, dev, rank, world=1):
     return sorted(wl, key=lambda w: ORDER.index(w.name) if w.name in ORDER else len(ORDER))
 
 
+def probe_workload(args, dev, name, tabs, n, seed, bufs):
+    """Row pre-probe: hash + row scan of every key against an
+    index holding all of them (a get-hit batch), `tabs` physical tabs per window.
+    Bytes per key: 16 key + 128 row + 16 record (+ the 2 MiB tab map once per
+    launch). probe16 (16 tabs: 256 MiB of rows, the size of the Infinity Cache)
+    is the cache-resident case; probe16_hbm (128 tabs: 2 GiB of rows) the HBM
+    regime. unique_bytes counts each distinct row once (keys + distinct rows +
+    records): the bytes HBM must deliver at least. probe16_hbm runs 256 keys
+    fewer, so its launch grid (which the PMC rows are matched on) differs."""
+    import torch
+
+    import sharedhashfile_amd as hb
+    from sharedhashfile_amd.keygen import device_random_bytes
+    from sharedhashfile_amd.rowindex import synthetic_index
+
+    keys = device_random_bytes(n * 16, seed, dev)
+    h = hb.hash_fixed(keys, 16)
+    tab_slot, rows, n_slots, placed = synthetic_index(h, tabs_per_win=tabs)
+    index = hb.RowIndex(n_slots, tab_slot, rows)
+    host_index = (tab_slot.cpu().numpy().view(np.uint32), rows.cpu().numpy(), n_slots)
+    # each key's row (slot * 512 + row) in key order: the probe's own row sequence, for its ceiling
+    h1 = h[:, 0]
+    rid = (((h1 & 0xFF) * tabs + ((h1 >> 16) & 0x7FF) % tabs) * 512 + ((h1 >> 32) & 0x1FF)).to(torch.int32)
+    distinct_rows = int(torch.unique(rid).numel())
+    bufs[name + "_rows"] = (rows, rid, n)
+    del h, tab_slot, h1
+    out = torch.empty((n, 4), dtype=torch.int32, device=dev)
+
+    def verify_probe(keys=keys, out=out, hx=host_index):
+        import torch as _t
+
+        from oracle.oracle_py import Oracle
+
+        o = Oracle()
+        idx = _sample_idx(n, VERIFY_SAMPLES, 16)
+        ti = _t.from_numpy(idx).to(dev)
+        k = keys.view(n, 16).index_select(0, ti).cpu().numpy()
+        want = o.probe(o.hash_fixed(k, 16), hx[0], hx[1], hx[2])
+        got = out.index_select(0, ti).cpu().numpy().view(np.uint32)
+        return bool(np.array_equal(got, want)), int(idx.size)
+
+    w = Workload(name, n, 16 + 128 + 16 + 4 * 256 * 2048 / n,
+                 [lambda k=keys, o=out, ix=index: hb.probe_fixed(ix, k, 16, out=o)],
+                 "k_fixed16<kOutProbe>", "%d fixed 16-B keys hashed and probed against a row index of "
+                 "%d slots (%.0f MiB, %s) holding %d of them; %d distinct rows"
+                 % (n, n_slots, n_slots / 16, "cache-resident" if n_slots * 65536 <= 256 << 20 else "HBM regime",
+                    placed, distinct_rows), verify_probe, grid_threads(name, n))
+    w.unique_bytes = 32.0 * n + 128.0 * distinct_rows
+    bufs[name + "_unique"] = w.unique_bytes
+    w.index = index
+    return w
+
+
 def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
     """The on-box ceilings (include/shf_hash_batch_ceiling.h), each on the
     buffers of the hashing line it bounds. `n` counts lanes; bytes_per_key is
@@ -483,6 +511,7 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
     import torch
 
     import sharedhashfile_amd as hb
+    from sharedhashfile_amd import bench_ceiling as bc
 
     wl = []
     if "ceil_copy" in only or "ceil_copy_hot" in only:
@@ -490,14 +519,14 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
         n = args.keys16
         if "ceil_copy" in only:
             wl.append(Workload("ceil_copy", n, 32,
-                               [ceil_launcher(hb, hb.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
+                               [ceil_launcher(hb, bc.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
                                 for k, o in pairs], "k_ceil_copy",
                                "16-B/lane copy in k_fixed16's shape over fixed16's %d rotating batches" % len(pairs),
                                grid=grid_threads("ceil_copy", n)))
         if "ceil_copy_hot" in only:
             k, o = pairs[0]
             wl.append(Workload("ceil_copy_hot", n, 32,
-                               [ceil_launcher(hb, hb.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
+                               [ceil_launcher(hb, bc.CEIL_COPY, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
                                "k_ceil_copy", "the same copy over fixed16_hot's single batch",
                                grid=grid_threads("ceil_copy_hot", n)))
     if "ceil_copynt" in only or "ceil_copynt_hot" in only:
@@ -505,17 +534,17 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
         n = args.keys16
         if "ceil_copynt" in only:
             wl.append(Workload("ceil_copynt", n, 32,
-                               [ceil_launcher(hb, hb.CEIL_COPY_NT, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
+                               [ceil_launcher(hb, bc.CEIL_COPY_NT, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)
                                 for k, o in pairs], "k_ceil_copyv<1>",
                                "the same copy with nontemporal stores (the fastest of tools/copy_sweep.py's variants) "
                                "over fixed16's %d rotating batches" % len(pairs), grid=grid_threads("ceil_copynt", n)))
         if "ceil_copynt_hot" in only:
             k, o = pairs[0]
             wl.append(Workload("ceil_copynt_hot", n, 32,
-                               [ceil_launcher(hb, hb.CEIL_COPY_NT, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
+                               [ceil_launcher(hb, bc.CEIL_COPY_NT, k.data_ptr(), 16 * n, None, o.data_ptr(), n, dev)],
                                "k_ceil_copyv<1>", "the same over fixed16_hot's single batch",
                                grid=grid_threads("ceil_copynt_hot", n)))
-    for name, kind, kern in (("ceil_copy_1b", hb.CEIL_COPY, "k_ceil_copy"), ("ceil_copynt_1b", hb.CEIL_COPY_NT,
+    for name, kind, kern in (("ceil_copy_1b", bc.CEIL_COPY, "k_ceil_copy"), ("ceil_copynt_1b", bc.CEIL_COPY_NT,
                                                                                 "k_ceil_copyv<1>")):
         if name not in only:
             continue
@@ -523,18 +552,21 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
         wl.append(Workload(name, n, 32,
                            [ceil_launcher(hb, kind, keys.data_ptr(), 16 * n, None, out.data_ptr(), n, dev)],
                            kern, "the same copy over shard1b's %d keys + hashes" % n, grid=grid_threads(name, n)))
-    if "ceil_probe_rows" in only and "probe_rows" in bufs:
-        rows, rid, n = bufs["probe_rows"]
+    for cname, pname in (("ceil_probe_rows", "probe16"), ("ceil_probe_rows_hbm", "probe16_hbm")):
+        if cname not in only or pname + "_rows" not in bufs:
+            continue
+        rows, rid, n = bufs[pname + "_rows"]
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         rid16 = torch.zeros((n, 4), dtype=torch.int32, device=dev)  # the row in the first word of a 16-B record
         rid16[:, 0] = rid
-        wl.append(Workload("ceil_probe_rows", n, 160,
-                           [ceil_launcher(hb, hb.CEIL_PROBE_ROWS, rows.data_ptr(), rows.numel(), rid16.data_ptr(),
+        wl.append(Workload(cname, n, 160,
+                           [ceil_launcher(hb, bc.CEIL_PROBE_ROWS, rows.data_ptr(), rows.numel(), rid16.data_ptr(),
                                           out.data_ptr(), n, dev)], "k_ceil_gather128<true>",
-                           "probe16's own row reads without the hash: a 16-B record per lane naming its key's 128-B "
+                           "%s's own row reads without the hash: a 16-B record per lane naming its key's 128-B "
                            "row (slot and row, in key order), the row fetched 8 lanes per row, a 16-B nt store: the "
-                           "probe's 160 B per key, %d lanes" % n, grid=grid_threads("ceil_probe_rows", n)))
+                           "probe's 160 B per key, %d lanes" % (pname, n), grid=grid_threads(cname, n)))
         wl[-1].keep = (rows, rid16, out)
+        wl[-1].unique_bytes = bufs.get(pname + "_unique")
     if {"ceil_read16", "ceil_read16nt", "ceil_read16w1"} & set(only):
         n = read16_lanes(args, only)
         if "fixed256" in bufs:
@@ -544,8 +576,8 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
             keys = torch.empty(n * 256, dtype=torch.uint8, device=dev)
             out = torch.empty((n, 2), dtype=torch.int64, device=dev)
             where = "a buffer of its own"
-        for name, kind, st in (("ceil_read16", hb.CEIL_READ16, "plain"), ("ceil_read16nt", hb.CEIL_READ16_NT, "nt"),
-                               ("ceil_read16w1", hb.CEIL_READ16_W1, "nt, one wave per workgroup")):
+        for name, kind, st in (("ceil_read16", bc.CEIL_READ16, "plain"), ("ceil_read16nt", bc.CEIL_READ16_NT, "nt"),
+                               ("ceil_read16w1", bc.CEIL_READ16_W1, "nt, one wave per workgroup")):
             if name not in only:
                 continue
             wl.append(Workload(name, n, 272,
@@ -560,7 +592,7 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
         idx = torch.randperm(n, device=dev, dtype=torch.int32)
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
         wl.append(Workload("ceil_gather128", n, 148,
-                           [ceil_launcher(hb, hb.CEIL_GATHER128, rows.data_ptr(), rows.numel(), idx.data_ptr(),
+                           [ceil_launcher(hb, bc.CEIL_GATHER128, rows.data_ptr(), rows.numel(), idx.data_ptr(),
                                           out.data_ptr(), n, dev)], "k_ceil_gather128",
                            "each of %d 128-B rows read once in random order, 8 lanes per row (the probe's row fetch) "
                            "+ 4-B index + 16-B store per lane" % n, grid=grid_threads("ceil_gather128", n)))
@@ -570,19 +602,19 @@ def ceiling_workloads(args, dev, only, bufs, fixed16_pairs):
         bs = [(torch.empty(16 * n + 16, dtype=torch.uint8, device=dev), torch.empty((n, 2), dtype=torch.int64,
                                                                                     device=dev)) for _ in range(2)]
         wl.append(Workload("ceil_stream16u", n, 32,
-                           [ceil_launcher(hb, hb.CEIL_STREAM16U, s_.data_ptr(), s_.numel(), None, o.data_ptr(), n, dev)
+                           [ceil_launcher(hb, bc.CEIL_STREAM16U, s_.data_ptr(), s_.numel(), None, o.data_ptr(), n, dev)
                             for s_, o in bs], "k_ceil_stream16u",
                            "16-B loads 7 bytes off alignment (the tab copy's record loads) + 16-B stores, %d lanes, "
                            "2 rotating buffers" % n, grid=grid_threads("ceil_stream16u", n)))
         wl[-1].keep = bs
-    for name, kind in (("ceil_valu_add", hb.CEIL_VALU_ADD), ("ceil_valu_mul", hb.CEIL_VALU_MUL)):
+    for name, kind in (("ceil_valu_add", bc.CEIL_VALU_ADD), ("ceil_valu_mul", bc.CEIL_VALU_MUL)):
         if name not in only:
             continue
         out = torch.empty((VALU_LANES, 2), dtype=torch.int64, device=dev)
         w = Workload(name, VALU_LANES, 16, [ceil_launcher(hb, kind, 1, VALU_ITERS, None, out.data_ptr(), VALU_LANES,
                                                           dev)], "k_ceil_valu",
                      "VALU-saturating launch: 8 independent %s chains x %d rounds per lane, %d lanes (32 waves/CU)"
-                     % ("v_add_u32" if kind == hb.CEIL_VALU_ADD else "v_mul_lo_u32", VALU_ITERS, VALU_LANES),
+                     % ("v_add_u32" if kind == bc.CEIL_VALU_ADD else "v_mul_lo_u32", VALU_ITERS, VALU_LANES),
                      grid=grid_threads(name, VALU_LANES))
         w.unit = "VALU lane-ops/s"
         w.ops_per_key = 8 * VALU_ITERS
@@ -955,7 +987,7 @@ PMC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"], RDREQ,
               ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                "GRBM_GUI_ACTIVE"]]
 PMC_SKIP = ("fixed16_hot", "shard1b", "ceil_copy_hot", "ceil_copy_1b", "ceil_copynt_hot", "ceil_copynt_1b",
-            "ceil_probe_rows")  # same kernels and grids as measured ones
+            "ceil_probe_rows", "ceil_probe_rows_hbm")  # same kernels and grids as measured ones
 
 
 def pmc_child_sizes(args, want):
@@ -964,6 +996,7 @@ def pmc_child_sizes(args, want):
     k256, kvar = min(args.keys256, 10_000_000), min(args.keysvar, 10_000_000)
     child = argparse.Namespace(keys256=k256, keys16=args.keys16)
     sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
+             "probe16_hbm": args.keys16 - 256,
              "tabpart": args.tab_jobs, "winorder": args.keys16, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
              "ceil_read16": read16_lanes(child, set(want)), "ceil_read16nt": read16_lanes(child, set(want)),
              "ceil_read16w1": read16_lanes(child, set(want)),
@@ -1028,6 +1061,8 @@ def collect_pmc(args, names):
                                          "--no-host-inclusive", "--traffic", "off", "--quiet", "--keys16",
                                          str(args.keys16), "--keys256", str(k256), "--keysvar", str(kvar),
                                          "--tab-jobs", str(args.tab_jobs), "--warmup-min-s", "0", "--gpus", "1",
+                                         "--probe-tabs", str(args.probe_tabs), "--probe-tabs-hbm",
+                                         str(args.probe_tabs_hbm),
                                          "--fixed-kernel", args.fixed_kernel, "--var-kernel", args.var_kernel]
         try:
             subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -1139,6 +1174,7 @@ def summarize(w, walls, devs, steps, keys_total):
         "kernel": w.kernel,
         "desc": w.desc,
         "enqueue_us_per_step": 1e6 * w.enqueue_s / steps,
+        "unique_gbs": (w.unique_bytes / per_launch / 1e9) if getattr(w, "unique_bytes", None) else None,
     }
 
 
@@ -1158,10 +1194,16 @@ def roofline_of(name, r, results, pmc, cal, args):
     if name.startswith("ceil_valu"):
         ro["bound"], ro["unit"], ro["peak"] = "valu", "lane-ops/s", None
         ro["achieved"], ro["frac"] = r["value"], None
+    if r.get("unique_gbs"):
+        # each distinct row counted once (keys + distinct rows + records): what HBM must deliver at least
+        ro["unique_gbs"] = round(r["unique_gbs"], 1)
+        ro["frac_unique"] = round(r["unique_gbs"] / HBM_PEAK_GBS, 4)
     if ceil is not None:
         ro["copy_ceiling"] = {"workload": ceil_name, "gbs": round(ceil["achieved_gbs"], 1),
                               "kernel_us": round(ceil["kernel_us"], 2)}
         ro["frac_of_copy_ceiling"] = round(r["achieved_gbs"] / ceil["achieved_gbs"], 4)
+        if r.get("unique_gbs") and ceil.get("unique_gbs"):
+            ro["frac_of_ceiling_unique"] = round(r["unique_gbs"] / ceil["unique_gbs"], 4)
     elif name in CEILING_OF:
         ro["frac_of_copy_ceiling"] = None
         ro["copy_ceiling"] = "%s not measured in this run" % " / ".join(CEILING_OF[name])
@@ -1264,6 +1306,108 @@ def build_line(args, world, n_gpus, shared, results, verified, per_rank, units, 
     return line
 
 
+LINE_MAX_BYTES = 4096  # the driver parses rank 0's stdout line from a ~10.7 KB stdout+stderr tail
+
+
+def _sig(x, d=4):
+    """x rounded to d significant digits (None and non-numbers pass through)."""
+    if not isinstance(x, (int, float)) or isinstance(x, bool) or x == 0:
+        return x
+    return float("%.*g" % (d, x))
+
+
+def compact_line(full, detail_path):
+    """The stdout line (<= LINE_MAX_BYTES): the contract's fields, a compact
+    roofline, cpu_baseline, host_inclusive and one short record per secondary
+    line. Everything else (PMC counters, calibration, descriptions, per-rank
+    records) stays in the detail file named by `detail`."""
+    ro = full["roofline"]
+    keep_ro = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_us",
+               "frac_of_copy_ceiling", "traffic_over_algorithmic", "valu_busy_range", "wait_frac", "limiter")
+    roof = {k: _sig(ro.get(k), 5) for k in keep_ro if k in ro}
+    if isinstance(ro.get("copy_ceiling"), dict):
+        roof["copy_ceiling_gbs"] = ro["copy_ceiling"]["gbs"]
+    if ro.get("algorithmic_bytes_per_launch"):
+        roof["algorithmic_bytes_per_launch"] = ro["algorithmic_bytes_per_launch"]
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "ranks", "steps", "warmup", "repeats",
+                                 "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype") if k in full}
+    line["value"] = _sig(line["value"], 6)
+    line["ms_per_step"] = _sig(line["ms_per_step"], 5)
+    line["value_min"], line["value_max"] = _sig(full["value_min"], 5), _sig(full["value_max"], 5)
+    line["data"] = "synthetic (device Philox key bytes, resident in HBM before timing)"
+    cfg = full["config"]
+    line["config"] = {"workload": "BASELINE configs[1]: %d x 16-B keys/GPU/step, MurmurHash3_x64_128 seed 12345 -> "
+                                  "SHF_HASH" % cfg["keys_per_gpu"],
+                      "keys_per_gpu": cfg["keys_per_gpu"], "key_len": cfg["key_len"],
+                      "parallelism": cfg["parallelism"]}
+    line["roofline"] = roof
+    line["verified"] = full.get("verified")
+    cpu = full.get("cpu_baseline")
+    if cpu:
+        c = {"value": _sig(cpu["value"], 5), "unit": cpu["unit"], "cores": cpu["cores"], "kind": cpu["kind"],
+             "sample": cpu["sample"][:160]}
+        mt = next((v for k, v in cpu.items() if k.startswith("threads")), None)
+        if mt:
+            c["multi"] = {"value": _sig(mt["value"], 5), "cores": mt["cores"]}
+        line["cpu_baseline"] = c
+    else:
+        line["cpu_baseline"] = None
+    hi = full.get("host_inclusive")
+    if hi:
+        line["host_inclusive"] = {k: _sig(v["value"], 4) for k, v in hi.items() if isinstance(v, dict)}
+        line["host_inclusive"]["verified"] = hi.get("verified")
+    sec, ceil = {}, {}
+    for name, s in (full.get("secondary") or {}).items():
+        r = s["roofline"]
+        if name.startswith("ceil_"):
+            ceil[name] = r["achieved"] if r.get("unit") == "GB/s" else _sig(s["value"], 4)
+            continue
+        e = {"value": _sig(s["value"], 5), "unit": s["unit"], "kernel_us": _sig(r.get("kernel_us"), 5),
+             "frac": r.get("frac"), "frac_of_ceiling": r.get("frac_of_copy_ceiling")}
+        if r.get("traffic_over_algorithmic") is not None:
+            e["traffic_x"] = r["traffic_over_algorithmic"]
+        for k in ("frac_unique", "frac_of_ceiling_unique"):
+            if k in r:
+                e[k] = r[k]
+        e["verified"] = (s.get("verified") or {}).get("ok")
+        if "scaling" in s:
+            e["scaling"] = s["scaling"]
+        sec[name] = e
+    line["secondary"] = sec
+    line["ceilings_gbs"] = ceil
+    if "slowest_over_fastest_rank" in full:
+        sp = full["slowest_over_fastest_rank"]
+        line["slowest_over_fastest_rank"] = {k: sp[k] for k in sp if not k.startswith("ceil_")}
+        line["barrier_backend"] = full.get("barrier_backend")
+    if full.get("rehearsal"):
+        line["rehearsal"] = True
+    line["detail"] = detail_path
+    # hard cap: drop the least important blocks until the line fits
+    for drop in ("ceilings_gbs", "slowest_over_fastest_rank", "host_inclusive"):
+        if len(json.dumps(line)) <= LINE_MAX_BYTES:
+            break
+        line.pop(drop, None)
+    while len(json.dumps(line)) > LINE_MAX_BYTES and line["secondary"]:
+        line["secondary"].popitem()
+    return line
+
+
+def detail_path_for(args, world):
+    return args.detail_out or os.path.join("gpurun_out", "bench_detail_n%d.json" % world)
+
+
+def write_detail(path, full):
+    """The full record (PMC counters, calibration, per-rank records) beside the line; best effort."""
+    try:
+        p = path if os.path.isabs(path) else os.path.join(ROOT, path)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            json.dump(full, f, indent=1)
+        return True
+    except OSError:
+        return False
+
+
 def run_rank(args):
     rank, world, local, local_world = dist_env()
     import torch
@@ -1296,9 +1440,8 @@ def run_rank(args):
         keys_total = (w.job_keys or w.n * world) * args.steps
         r = results[w.name] = summarize(w, walls, devs, args.steps, keys_total)
         mine["kernel_us"][w.name] = round(float(np.median(devs_local)) * 1e6, 2)
-        log(args, "[bench] %s: %.4g %s (min %.4g, max %.4g), %.1f us/launch, %.0f GB/s, enqueue %.1f us/step"
-            % (w.name, r["value"], getattr(w, "unit", "keys/s"), r["value_min"], r["value_max"], r["kernel_us"],
-               r["achieved_gbs"], r["enqueue_us_per_step"]))
+        log(args, "[bench] %s %.4g %s %.1fus %.0fGB/s" % (w.name, r["value"], getattr(w, "unit", "keys/s"),
+                                                        r["kernel_us"], r["achieved_gbs"]))
         if not args.no_verify and w.verify is not None:
             try:
                 ok, checked = w.verify()
@@ -1334,8 +1477,12 @@ def run_rank(args):
         cpu = cpu_baseline(args) if world == 1 and not args.no_cpu else None
         host_inc = time_host_inclusive(args, dev) if world == 1 and not args.no_host_inclusive else None
         units = {w.name: getattr(w, "unit", "keys/s") for w in wl}
-        line = build_line(args, world, n_gpus, shared, results, verified, per_rank, units, pmc, pmc_note, cpu,
+        full = build_line(args, world, n_gpus, shared, results, verified, per_rank, units, pmc, pmc_note, cpu,
                           host_inc, shards)
+        dpath = detail_path_for(args, world)
+        if not write_detail(dpath, full):
+            dpath = None
+        line = compact_line(full, dpath)
         os.write(args.json_fd, (json.dumps(line) + "\n").encode())
     if dist:
         dist.barrier()

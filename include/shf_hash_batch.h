@@ -320,10 +320,13 @@ SHF_HB_API int shf_tab_part_redirect(uint16_t *map, uint32_t tab_old, uint32_t t
  * n < 2^32 (32-bit indices); n == 0 sets win_start to zeros.
  *
  * _async: every pointer on the device, enqueued on hip_stream; d_workspace of
- * at least shf_win_order_workspace_bytes(n) bytes, in use until the call has
- * run on the stream. Not reentrant on one workspace.
- * shf_win_order: synchronous; mem = SHF_HASH_MEM_DEVICE (device pointers) or
- * SHF_HASH_MEM_HOST (host pointers, copied through device buffers). */
+ * at least shf_win_order_workspace_bytes(n) bytes, 16-B aligned (else
+ * SHF_HB_ERR_ARG), in use until the call has run on the stream. Not reentrant
+ * on one workspace.
+ * shf_win_order: synchronous; mem = SHF_HASH_MEM_DEVICE (device pointers; runs
+ * on the null stream, after the caller's work there, like the synchronous
+ * hashing calls) or SHF_HASH_MEM_HOST (host pointers, copied through device
+ * buffers). Its workspace is kept per thread and device across calls. */
 SHF_HB_API size_t shf_win_order_workspace_bytes(uint64_t n);
 SHF_HB_API int shf_win_order_async(const shf_hash128 *d_hashes, uint64_t n, uint32_t *d_perm,
                                    uint32_t *d_win_start, void *d_workspace, size_t workspace_bytes,

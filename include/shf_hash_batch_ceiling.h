@@ -1,6 +1,8 @@
 /*
- * shf_hash_batch_ceiling.h -- measurement kernels shipped with
- * libshf_hash_batch.so: the on-box HBM ceilings that bench.py reports each
+ * shf_hash_batch_ceiling.h -- measurement kernels of the bench-only library
+ * libshf_hb_bench.so (NOT the product libshf_hash_batch.so, which neither
+ * contains nor exports them; only bench.py, tools/ and the tests load this
+ * one): the on-box HBM ceilings that bench.py reports each
  * hashing kernel against (roofline.frac_of_copy_ceiling), and the access
  * patterns that calibrate rocprofv3's FETCH_SIZE for the probe's row gathers
  * and the tab copy's unaligned loads. They replace no reference interface:
@@ -23,7 +25,7 @@ extern "C" {
 #define SHF_HB_CEIL_READ16 1    /* 16 x 16-B nt loads (a wave reads one contiguous 16 KiB) + 16-B store: 272 B;
                                    n a multiple of 64, src_bytes >= 256 n */
 #define SHF_HB_CEIL_GATHER128 2 /* 4-B idx[i], the 128-B row src[128 idx[i] ..], fetched 8 lanes per row like the
-                                   row pre-probe, + 16-B store: 148 B; every idx[i] < src_bytes / 128 (caller's duty) */
+                                   row pre-probe, + 16-B store: 148 B; an idx[i] >= src_bytes / 128 reads row 0 */
 #define SHF_HB_CEIL_STREAM16U 3 /* 16-B load at src + 16 i + shift (byte-unaligned: shift = 7 for an aligned src)
                                    + 16-B store: 32 B; src_bytes >= 16 n + 16 */
 #define SHF_HB_CEIL_VALU_ADD 4  /* no loads: 8 independent v_add_u32 chains per lane, src_bytes rounds (the loop

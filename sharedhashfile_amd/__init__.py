@@ -102,24 +102,7 @@ _SIGS = {
     "shf_hash_batch_last_hip_error": [],
     "shf_hash_batch_strerror": [_INT],
     "shf_hash_batch_version": [],
-    "shf_hb_ceiling_async": [_INT, _VP, _U64, _VP, _VP, _U64, _VP],  # include/shf_hash_batch_ceiling.h
 }
-
-# include/shf_hash_batch_ceiling.h: the on-box HBM ceilings bench.py measures
-CEIL_COPY = 0
-CEIL_READ16 = 1
-CEIL_GATHER128 = 2
-CEIL_STREAM16U = 3
-CEIL_VALU_ADD = 4
-CEIL_VALU_MUL = 5
-CEIL_COPY4 = 6
-CEIL_COPY_PLAIN = 7
-CEIL_COPY_NT = 8
-CEIL_COPY_SLEEP = 9
-CEIL_COPY2 = 10
-CEIL_READ16_NT = 11
-CEIL_READ16_W1 = 12
-CEIL_PROBE_ROWS = 13
 
 
 _RESTYPES = {"shf_hash_batch_strerror": ctypes.c_char_p, "shf_hash_batch_version": ctypes.c_char_p,
@@ -488,7 +471,8 @@ def win_order(hashes, perm=None, win_start=None, workspace=None, stream=None):
     _require_out(win_start, (257,), (torch.int32,), dev)
     lib = load()
     need = lib.shf_win_order_workspace_bytes(n)
-    if workspace is None:
+    own_ws = workspace is None
+    if own_ws:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
     _require_cuda_u8(workspace, "workspace")
     with _on(hashes):
@@ -496,6 +480,10 @@ def win_order(hashes, perm=None, win_start=None, workspace=None, stream=None):
                                      ctypes.c_void_p(win_start.data_ptr()), ctypes.c_void_p(workspace.data_ptr()),
                                      workspace.numel(), _stream_handle(stream))
     _check(rc, "shf_win_order_async")
+    if stream is not None and own_ws:
+        # the kernels still read the scratch on `stream` after this returns: keep the
+        # caching allocator from handing its bytes out before that stream gets there
+        workspace.record_stream(stream)
     return perm, win_start
 
 

@@ -4,7 +4,10 @@
 
 The library is a plain hipcc shared object, built in-tree so it travels to the
 GPU box with the repository snapshot:
-    sharedhashfile_amd/libshf_hash_batch.so
+    sharedhashfile_amd/libshf_hash_batch.so   the product (include/shf_hash_batch.h)
+    sharedhashfile_amd/libshf_hb_bench.so     bench-only ceiling kernels
+                                              (include/shf_hash_batch_ceiling.h), never
+                                              linked into the product
 """
 import os
 import subprocess
@@ -14,7 +17,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libshf_hash_batch.so")
-SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip", "hbm_ceiling.hip", "win_order.hip"]
+SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip", "win_order.hip"]
+BENCH_CSRC = os.path.join(PKG, "csrc_bench")
+BENCH_LIB = os.path.join(PKG, "libshf_hb_bench.so")
+BENCH_SOURCES = ["hbm_ceiling.hip"]
 HEADERS = ["kernels.h", "murmur3_mix.h"]
 ARCH = "gfx950"
 
@@ -33,19 +39,28 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force=False, verbose=True):
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps += [os.path.join(ROOT, "include", h) for h in ("shf_hash_batch.h", "shf_hash_batch_ceiling.h")]
-    if not force and not _stale(LIB, deps):
-        return LIB
+def _hipcc_shared(sources, headers, out, force, verbose):
+    if not force and not _stale(out, sources + headers):
+        return out
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fvisibility=hidden", "-Wall", "-I" + os.path.join(ROOT, "include")]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-o", LIB + ".tmp"]
+    cmd += sources + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_library(force=False, verbose=True):
+    """The product library, then the bench-only ceiling library beside it."""
+    inc = os.path.join(ROOT, "include")
+    _hipcc_shared([os.path.join(CSRC, s) for s in SOURCES],
+                  [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(inc, "shf_hash_batch.h")], LIB, force,
+                  verbose)
+    _hipcc_shared([os.path.join(BENCH_CSRC, s) for s in BENCH_SOURCES],
+                  [os.path.join(inc, h) for h in ("shf_hash_batch.h", "shf_hash_batch_ceiling.h")], BENCH_LIB, force,
+                  verbose)
     return LIB
 
 

@@ -132,6 +132,8 @@ struct DevCtx {
   // each synchronous call.
   uint32_t* d_status = nullptr;
   uint32_t* h_status = nullptr;  // pinned, 1 word
+  void* d_win_ws = nullptr;      // shf_win_order's workspace, kept across calls (grows only)
+  size_t win_ws_cap = 0;
 };
 
 void release_ctx(DevCtx* c);
@@ -220,6 +222,7 @@ void release_ctx(DevCtx* c) {
   }
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);
+  if (c->d_win_ws) (void)hipFree(c->d_win_ws);
   (void)hipGetLastError();
   (void)hipSetDevice(prev);
   delete c;
@@ -249,6 +252,22 @@ int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys, int slots) {
   c->in_cap = ib;
   c->key_cap = kc;
   c->n_staged = ns;
+  return SHF_HB_OK;
+}
+
+// shf_win_order's workspace: grown when a batch needs more, else reused (a hipFree per call
+// would synchronise the device every batch). Every stream of the context is idle first.
+int ensure_win_ws(DevCtx* c, size_t bytes, void** out) {
+  if (bytes > c->win_ws_cap) {
+    for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
+    HB_TRY(hipStreamSynchronize(nullptr));
+    if (c->d_win_ws) (void)hipFree(c->d_win_ws);
+    c->d_win_ws = nullptr;
+    c->win_ws_cap = 0;
+    HB_TRY(hipMalloc(&c->d_win_ws, bytes));
+    c->win_ws_cap = bytes;
+  }
+  *out = c->d_win_ws;
   return SHF_HB_OK;
 }
 
@@ -1229,6 +1248,7 @@ int shf_win_order_async(const shf_hash128* d_hashes, uint64_t n, uint32_t* d_per
   if (n > 0xffffffffull) return SHF_HB_ERR_ARG;
   if (n && (!d_hashes || !d_perm || !d_workspace || workspace_bytes < shfhb::win_order_workspace_bytes(n)))
     return SHF_HB_ERR_ARG;
+  if (((uintptr_t)d_workspace & 15u) != 0) return SHF_HB_ERR_ARG;  // the window bytes move 16 B at a time
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -1243,12 +1263,15 @@ int shf_win_order(const shf_hash128* hashes, uint64_t n, uint32_t* perm, uint32_
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  hipStream_t st = c->st[0];
+  // device memory: on the null stream, as the synchronous hashing calls do, so the order
+  // runs after whatever the caller enqueued there (e.g. the hashes it orders)
+  hipStream_t st = mem == SHF_HASH_MEM_DEVICE ? nullptr : c->st[0];
   const size_t ws = (size_t)shfhb::win_order_workspace_bytes(n), ws_start = 257u * sizeof(uint32_t);
-  TmpDevBuf d_ws, d_h, d_p, d_s;
-  HB_TRY(hipMalloc(&d_ws.p, ws));
+  void* d_ws = nullptr;
+  if ((rc = ensure_win_ws(c, ws, &d_ws))) return rc;
+  TmpDevBuf d_h, d_p, d_s;
   if (mem == SHF_HASH_MEM_DEVICE) {
-    HB_TRY(shfhb::launch_win_order(hashes, n, perm, win_start, d_ws.p, st));
+    HB_TRY(shfhb::launch_win_order(hashes, n, perm, win_start, d_ws, st));
     HB_TRY(hipStreamSynchronize(st));
     return SHF_HB_OK;
   }
@@ -1258,7 +1281,7 @@ int shf_win_order(const shf_hash128* hashes, uint64_t n, uint32_t* perm, uint32_
     HB_TRY(hipMemcpyAsync(d_h.p, hashes, n * sizeof(shf_hash128), hipMemcpyHostToDevice, st));
   }
   if (win_start) HB_TRY(hipMalloc(&d_s.p, ws_start));
-  HB_TRY(shfhb::launch_win_order(d_h.p, n, (uint32_t*)d_p.p, (uint32_t*)d_s.p, d_ws.p, st));
+  HB_TRY(shfhb::launch_win_order(d_h.p, n, (uint32_t*)d_p.p, (uint32_t*)d_s.p, d_ws, st));
   if (n) HB_TRY(hipMemcpyAsync(perm, d_p.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   if (win_start) HB_TRY(hipMemcpyAsync(win_start, d_s.p, ws_start, hipMemcpyDeviceToHost, st));
   HB_TRY(hipStreamSynchronize(st));

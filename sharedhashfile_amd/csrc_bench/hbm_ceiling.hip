@@ -1,6 +1,8 @@
 // Measurement kernels: the HBM ceilings bench.py divides the hashing kernels'
 // rates by, measured on the same box in the same run (include/shf_hash_batch_ceiling.h).
-// Not part of the hashing path: each kernel moves exactly the bytes of one
+// Built into its own library, libshf_hb_bench.so, which only bench.py, tools/ and
+// the tests load: the product library libshf_hash_batch.so does not contain or
+// export them. Not part of the hashing path: each kernel moves exactly the bytes of one
 // hashing kernel's access pattern and computes nothing but an XOR fold.
 //
 //   k_ceil_copy      lane i: one 16-B nontemporal load of src[i], one 16-B store
@@ -113,8 +115,9 @@ __global__ __launch_bounds__(BLOCK) void k_ceil_read16(const u32x4* __restrict__
 // IDX16: the index arrives as 16-B records (the row index in the first word), as
 // the probe reads a 16-B key per lane, and the result is stored nontemporally as
 // the probe stores its record: SHF_HB_CEIL_PROBE_ROWS, 160 B per lane.
+// An index naming a row past n_rows reads row 0 instead (never past src).
 template <bool IDX16>
-__global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __restrict__ rows,
+__global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __restrict__ rows, uint32_t n_rows,
                                                            const uint32_t* __restrict__ idx, u32x4* __restrict__ dst,
                                                            uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -123,6 +126,7 @@ __global__ __launch_bounds__(kBlock) void k_ceil_gather128(const uint8_t* __rest
   if (i < n) {
     if constexpr (IDX16) r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(idx) + i).x;
     else r = __builtin_nontemporal_load(&idx[i]);
+    r = r < n_rows ? r : 0u;
   }
   u32x4 g[8];
 #pragma unroll
@@ -218,18 +222,20 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
                            (const u32x4*)d_src, (u32x4*)d_dst, n);
       break;
     case SHF_HB_CEIL_GATHER128:
-    case SHF_HB_CEIL_PROBE_ROWS:
-      // every idx[i] must name a row inside src: checked by the caller's construction (a permutation
-      // of src_bytes / 128 rows, or the probe's own rows), not here -- the launcher cannot read device memory
+    case SHF_HB_CEIL_PROBE_ROWS: {
+      // an idx[i] >= src_bytes / 128 is clamped to row 0 by the kernel (the launcher cannot read device memory)
       if (!al16 || !d_idx || src_bytes < 128u || src_bytes / 128u > 0xffffffffull) return SHF_HB_ERR_ARG;
+      const uint32_t n_rows = (uint32_t)(src_bytes / 128u);
       if (kind == SHF_HB_CEIL_GATHER128)
-        hipLaunchKernelGGL(k_ceil_gather128<false>, grid, block, 0, st, (const uint8_t*)d_src, d_idx, (u32x4*)d_dst, n);
+        hipLaunchKernelGGL(k_ceil_gather128<false>, grid, block, 0, st, (const uint8_t*)d_src, n_rows, d_idx,
+                           (u32x4*)d_dst, n);
       else if ((reinterpret_cast<uintptr_t>(d_idx) & 15u) != 0)
         return SHF_HB_ERR_ARG;
       else  // with the probe kernel's 32 KiB of LDS per 256-thread workgroup, hence its occupancy
-        hipLaunchKernelGGL(k_ceil_gather128<true>, grid, block, 32u * 1024u, st, (const uint8_t*)d_src, d_idx,
-                           (u32x4*)d_dst, n);
+        hipLaunchKernelGGL(k_ceil_gather128<true>, grid, block, 32u * 1024u, st, (const uint8_t*)d_src, n_rows,
+                           d_idx, (u32x4*)d_dst, n);
       break;
+    }
     case SHF_HB_CEIL_STREAM16U: {
       const uint32_t shift = (uint32_t)(((uintptr_t)d_src) & 15u) ? 0u : 7u;  // aligned base: read 7 bytes in
       if (src_bytes < 16u * n + 16u) return SHF_HB_ERR_ARG;

@@ -27,17 +27,31 @@ def _has_gpu():
 def test_library_exports_every_header_symbol(hb):
     declared = hbmod.header_functions()
     assert len(declared) >= 14
-    # every C header of include/ whose functions the library defines (the .h/.hpp seam headers are static inline)
-    ceiling = hbmod.header_functions(os.path.join(ROOT, "include", "shf_hash_batch_ceiling.h"))
-    assert ceiling == ["shf_hb_ceiling_async"]
-    declared = declared + ceiling
+    # the product library exports exactly include/shf_hash_batch.h (the .h/.hpp seam headers are static inline)
     out = subprocess.check_output(["nm", "-D", "--defined-only", hbmod.LIB_PATH]).decode()
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     missing = [f for f in declared if f not in exported]
     assert not missing, missing
-    # nothing else leaks out of the shared object (hidden visibility)
-    extra = sorted(s for s in exported if not s.startswith("shf_"))
+    # nothing else leaks out of the shared object (hidden visibility), measurement kernels included
+    extra = sorted(s for s in exported if s not in declared)
     assert not extra, extra
+    assert not any(s.startswith("shf_hb_ceiling") for s in exported)
+    assert "k_ceil" not in subprocess.check_output(["nm", "-C", hbmod.LIB_PATH]).decode()
+
+
+def test_bench_library_is_separate():
+    """The ceiling kernels (include/shf_hash_batch_ceiling.h) live in the
+    bench-only libshf_hb_bench.so, which exports only them."""
+    from sharedhashfile_amd import bench_ceiling
+
+    ceiling = hbmod.header_functions(os.path.join(ROOT, "include", "shf_hash_batch_ceiling.h"))
+    assert ceiling == ["shf_hb_ceiling_async"]
+    hbmod.load()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", bench_ceiling.BENCH_LIB_PATH]).decode()
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert exported == set(ceiling), exported
+    assert bench_ceiling.load().shf_hb_ceiling_async(0, None, 0, None, None, 0, None) == hbmod.OK  # n == 0
+    assert bench_ceiling.load().shf_hb_ceiling_async(99, 16, 16, None, 16, 1, None) == hbmod.ERR_ARG
 
 
 def test_header_compiles_as_c():
@@ -160,7 +174,8 @@ def test_missing_library_raises(tmp_path):
         hbmod.load(str(tmp_path / "nope.so"))
 
 
-@pytest.mark.parametrize("source,min_kernels", [("kernels.hip", 30), ("tab_copy.hip", 1), ("hbm_ceiling.hip", 4), ("win_order.hip", 3)])
+@pytest.mark.parametrize("source,min_kernels", [("kernels.hip", 30), ("tab_copy.hip", 1),
+                                                ("../csrc_bench/hbm_ceiling.hip", 4), ("win_order.hip", 3)])
 def test_kernels_compile_without_scratch(source, min_kernels):
     """Every kernel instantiation fits in registers (no scratch spills), as
     reported by hipcc's resource-usage remarks for gfx950."""

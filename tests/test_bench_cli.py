@@ -187,3 +187,61 @@ def test_multi_kernel_workload_counters_sum_over_its_kernels():
     m = bench.pmc_medians(vals["winorder"])
     assert m["FETCH_SIZE"] == 101.0 + 11.0 + 6.0  # the three kernels' medians, summed
     assert bench.pmc_medians(vals["fixed16"]) == {"FETCH_SIZE": 7.0}
+
+
+def _full_results():
+    names = bench.HASH_WORKLOADS + bench.CEIL_WORKLOADS
+    return {n: _fake_result(n, 6000.0 + i, us=50.0 + i) for i, n in enumerate(names)}
+
+
+def _compact(world, cpu=None, host_inc=None):
+    results = _full_results()
+    verified = {n: {"ok": True, "samples_per_rank": 20002} for n in bench.HASH_WORKLOADS}
+    per_rank = [{"rank": r, "device": r, "device_name": "AMD Instinct MI355X", "shard": [r * 125_000_000,
+                                                                                        (r + 1) * 125_000_000],
+                 "kernel_us": {n: 50.0 + r for n in results}, "verified": {n: True for n in verified}}
+                for r in range(world)] if world > 1 else None
+    units = {n: "lanes/s" if n.startswith("ceil_") else "keys/s" for n in results}
+    full = bench.build_line(_args(), world, world, False, results, verified, per_rank, units, None, "not collected",
+                            cpu, host_inc, [[0, 1]] * world)
+    return full, bench.compact_line(full, "gpurun_out/bench_detail_n%d.json" % world)
+
+
+def test_stdout_line_fits_the_driver_tail_at_one_and_eight_ranks():
+    """BENCH_r03's 28.8-KB line overflowed the driver's ~10.7-KB tail and went
+    unparsed: the stdout line is capped at 4 KB, the rest goes to the detail file."""
+    cpu = {"value": 1.476e8, "unit": "keys/s", "cores": 1, "kind": "reference", "sample": "x" * 400,
+           "host_cpus": {"visible": 256}, "threads16": {"value": 2.1e9, "unit": "keys/s", "cores": 16, "sample": "y"}}
+    hi = {"unit": "keys/s", "note": "n" * 500, "verified": True}
+    for k in ("fixed16_pageable", "fixed16_pageable_staged", "fixed16_pinned", "fixed16_pinned_staged",
+              "var_pageable", "var_pinned"):
+        hi[k] = {"value": 2.5e9, "value_min": 2.4e9, "value_max": 2.6e9, "repeats": 5}
+    for world in (1, 8):
+        full, line = _compact(world, cpu if world == 1 else None, hi if world == 1 else None)
+        s = bench.json.dumps(line)
+        assert len(s) <= bench.LINE_MAX_BYTES, (world, len(s))
+        back = bench.json.loads(s)
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+                  "roofline", "cpu_baseline", "higher_is_better", "scaling", "vs_baseline"):
+            assert k in back, k
+        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+            assert k in back["roofline"], k
+        assert back["n_gpus"] == world and back["detail"].endswith("n%d.json" % world)
+        # every hashing line of the run keeps a short record
+        assert set(back["secondary"]) == set(bench.HASH_WORKLOADS) - {"fixed16"}
+        assert all(set(e) >= {"value", "frac", "frac_of_ceiling", "verified"} for e in back["secondary"].values())
+        assert len(bench.json.dumps(full)) > len(s)  # the detail record keeps what the line drops
+    _, line1 = _compact(1, cpu, hi)
+    assert line1["cpu_baseline"]["kind"] == "reference" and line1["cpu_baseline"]["multi"]["cores"] == 16
+    assert line1["host_inclusive"]["fixed16_pinned"] == 2.5e9
+    _, line8 = _compact(8)
+    assert "per_rank" not in line8 and line8["slowest_over_fastest_rank"]["fixed16"] == round(57.0 / 50.0, 4)
+
+
+def test_compact_line_trims_to_the_cap_whatever_the_detail():
+    full, _ = _compact(1)
+    for i in range(200):  # far more secondary lines than any run has
+        full["secondary"]["extra%03d" % i] = dict(full["secondary"]["var"])
+    line = bench.compact_line(full, "d.json")
+    assert len(bench.json.dumps(line)) <= bench.LINE_MAX_BYTES
+    assert line["roofline"]["frac"] == full["roofline"]["frac"]

@@ -179,8 +179,33 @@ def test_win_order_rejects_bad_arguments(hb, dev):
         assert lib.shf_win_order_async(vp(h), 10000, None, None, vp(ws), need, None) == hb.ERR_ARG
         assert lib.shf_win_order_async(vp(h), 1 << 32, vp(p), None, vp(ws), need, None) == hb.ERR_ARG
         assert lib.shf_win_order(vp(h), 10000, vp(p), None, 7) == hb.ERR_ARG
+        ws2 = torch.empty(need + 16, dtype=torch.uint8, device=dev)
+        assert lib.shf_win_order_async(vp(h), 10000, vp(p), None, ctypes.c_void_p(ws2.data_ptr() + 4), need, None) \
+            == hb.ERR_ARG  # a workspace slice off 16-B alignment
         assert lib.shf_win_order_async(vp(h), 10000, vp(p), None, vp(ws), need, None) == hb.OK
     torch.cuda.synchronize(dev)
+
+
+@pytest.mark.gpu
+def test_win_order_on_a_side_stream_outside_its_context(hb, dev, oracle):
+    """stream= given without `with torch.cuda.stream(s)`: the wrapper's own
+    workspace stays reserved for that stream until its kernels ran,
+    so churning the allocator on the current stream meanwhile cannot corrupt it."""
+    import torch
+
+    rng = np.random.default_rng(31)
+    hn = rng.integers(0, 2**63, size=(300_000, 2), dtype=np.int64)
+    h = torch.from_numpy(hn).to(dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    want_p, want_s = oracle.win_order(hn.view(np.uint64))
+    for _ in range(3):
+        perm, ws = hb.win_order(h, stream=s)
+        junk = [torch.full((1 << 20,), 7, dtype=torch.uint8, device=dev) for _ in range(8)]  # reuse freed blocks
+        del junk
+        s.synchronize()
+        np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), want_p)
+        np.testing.assert_array_equal(ws.cpu().numpy().view(np.uint32), want_s)
 
 
 @pytest.mark.gpu

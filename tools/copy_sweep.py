@@ -26,7 +26,10 @@ def main():
     from sharedhashfile_amd.keygen import device_random_bytes
 
     dev = torch.device("cuda:0")
+    from sharedhashfile_amd import bench_ceiling
+
     lib = hb.load()
+    blib = bench_ceiling.load()
     n = a.n
     pairs = [(device_random_bytes(16 * n, 100 + b, dev), torch.empty((n, 2), dtype=torch.int64, device=dev))
              for b in range(4)]
@@ -34,7 +37,7 @@ def main():
     variants = {}
     for name, kind in (("copy_nt_ld", 0), ("copy4", 6), ("copy_plain", 7), ("copy_nt_ldst", 8), ("copy_sleep", 9),
                        ("copy2", 10)):
-        variants[name] = (lambda kind: lambda k, o: lib.shf_hb_ceiling_async(kind, k.data_ptr(), 16 * n, None,
+        variants[name] = (lambda kind: lambda k, o: blib.shf_hb_ceiling_async(kind, k.data_ptr(), 16 * n, None,
                                                                               o.data_ptr(), n, st()))(kind)
     variants["torch_copy_"] = lambda k, o: (o.view(torch.uint8).view(-1).copy_(k), 0)[1]
     variants["hash_k_fixed16"] = lambda k, o: lib.shf_hash_batch_fixed_kernel_async(k.data_ptr(), 16, n, 12345,
