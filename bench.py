@@ -1372,6 +1372,8 @@ def compact_line(full, detail_path):
         e["verified"] = (s.get("verified") or {}).get("ok")
         if "scaling" in s:
             e["scaling"] = s["scaling"]
+        if s.get("shards"):
+            e["shards"] = s["shards"]
         sec[name] = e
     line["secondary"] = sec
     line["ceilings_gbs"] = ceil

@@ -43,11 +43,13 @@ def test_two_ranks_refused_on_one_gpu():
     assert p.stdout.strip() == ""
 
 
-def test_two_rank_rehearsal_shards_configs4():
-    p = _run(["--allow-shared-gpu"])
+def test_two_rank_rehearsal_shards_configs4(tmp_path):
+    detail = str(tmp_path / "detail.json")
+    p = _run(["--allow-shared-gpu", "--detail-out", detail])
     assert p.returncode == 0, p.stderr[-3000:]
     out = p.stdout.strip().splitlines()
     assert len(out) == 1, out  # stdout is the JSON line alone (gloo's notices and the like go to stderr)
+    assert len(out[0]) <= 4096  # what the driver's tail can hold
     line = json.loads(out[0])
     ndev = torch.cuda.device_count()
     assert line["ranks"] == 2
@@ -56,12 +58,15 @@ def test_two_rank_rehearsal_shards_configs4():
     sh = line["secondary"]["shard1b"]
     assert sh["scaling"] == "strong"
     assert sh["shards"] == [[0, 500_000_000], [500_000_000, 1_000_000_000]]
-    assert sh["verified"]["ok"] is True and sh["verified"]["samples_per_rank"] >= 20000
+    assert sh["verified"] is True
     assert line["verified"] is True
-    # value = all ranks' keys / max-over-ranks time
-    assert line["value"] == pytest.approx(2 * 1_000_000 * 5 / (line["ms_per_step"] * 5 / 1e3), rel=1e-6)
-    # per-rank evidence: device, own kernel times and verdicts, the shard each took
-    pr = line["per_rank"]
+    # value = all ranks' keys / max-over-ranks time (the line rounds to 6 digits)
+    assert line["value"] == pytest.approx(2 * 1_000_000 * 5 / (line["ms_per_step"] * 5 / 1e3), rel=1e-4)
+    # the detail file the line names: per-rank evidence (device, own kernel times and verdicts, shards)
+    assert line["detail"] == detail
+    full = json.load(open(detail))
+    assert full["secondary"]["shard1b"]["verified"]["samples_per_rank"] >= 20000
+    pr = full["per_rank"]
     assert [p["rank"] for p in pr] == [0, 1]
     assert [p["device"] for p in pr] == [r % max(1, ndev) for r in range(2)]
     assert all(p["kernel_us"]["fixed16"] > 0 and p["kernel_us"]["shard1b"] > 0 for p in pr)
@@ -90,5 +95,5 @@ def test_two_rank_rehearsal_under_torch_distributed_run():
     line = json.loads(lines[0])
     assert line["ranks"] == 2 and line["verified"] is True
     assert line["secondary"]["shard1b"]["shards"] == [[0, 500_000_000], [500_000_000, 1_000_000_000]]
-    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
+    assert [r["rank"] for r in json.load(open(os.path.join(ROOT, line["detail"])))["per_rank"]] == [0, 1]
     assert line["barrier_backend"] == "gloo"
