@@ -79,12 +79,13 @@ KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1
                "ceil_valu_mul": "k_ceil_valu<1>", "ceil_copynt": "k_ceil_copyv<1>(", "ceil_copynt_hot": "k_ceil_copyv<1>(",
                "ceil_copynt_1b": "k_ceil_copyv<1>(", "ceil_probe_rows": "k_ceil_gather128<true>",
                "ceil_probe_rows_hbm": "k_ceil_gather128<true>",
-               "winorder": "k_wo_"}
+               "winorder": "k_wo_", "hashwin16": "k_fixed16_win"}
 # workloads whose one call is several kernels: their counters are summed over the kernels
 # (each kernel's median per launch), so traffic covers the whole call
-MULTI_KERNEL = {"winorder": ["k_wo_hist", "k_wo_scan", "k_wo_scatter"]}
+MULTI_KERNEL = {"winorder": ["k_wo_hist", "k_wo_scan_rows", "k_wo_scatter"],
+                "hashwin16": ["k_fixed16_win", "k_wo_scan_rows", "k_wo_scatter"]}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "probe16_hbm", "tabpart",
-                  "winorder"]
+                  "winorder", "hashwin16"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
                   "ceil_read16", "ceil_read16nt", "ceil_read16w1", "ceil_probe_rows", "ceil_probe_rows_hbm", "ceil_gather128", "ceil_stream16u", "ceil_valu_add",
                   "ceil_valu_mul"]
@@ -95,17 +96,18 @@ CEILING_OF = {"fixed16": ["ceil_copy", "ceil_copynt"], "fixed16_hot": ["ceil_cop
               "shard1b": ["ceil_copy_1b", "ceil_copynt_1b"], "fixed256": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
               "var": ["ceil_read16", "ceil_read16nt", "ceil_read16w1"],
               "probe16": ["ceil_probe_rows"], "probe16_hbm": ["ceil_probe_rows_hbm"], "tabpart": ["ceil_copy", "ceil_copynt"],
-              "winorder": ["ceil_copy", "ceil_copynt"]}
+              "winorder": ["ceil_copy", "ceil_copynt"], "hashwin16": ["ceil_copy", "ceil_copynt"]}
 # timing order: each ceiling right after the line it bounds (same buffers, same thermal state)
 ORDER = ["fixed16", "ceil_copy", "ceil_copynt", "fixed16_hot", "ceil_copy_hot", "ceil_copynt_hot", "shard1b",
          "ceil_copy_1b", "ceil_copynt_1b", "fixed256", "ceil_read16", "ceil_read16nt", "ceil_read16w1", "var", "probe16", "ceil_probe_rows",
          "probe16_hbm", "ceil_probe_rows_hbm",
-         "ceil_gather128", "tabpart", "ceil_stream16u", "winorder", "ceil_valu_add", "ceil_valu_mul"]
+         "ceil_gather128", "tabpart", "ceil_stream16u", "winorder", "hashwin16", "ceil_valu_add",
+         "ceil_valu_mul"]
 # the pattern whose known byte count calibrates each line's FETCH_SIZE
 FETCH_CAL_OF = {"fixed16": "ceil_copy", "fixed16_hot": "ceil_copy", "shard1b": "ceil_copy",
                 "fixed256": "ceil_read16", "var": "ceil_read16", "probe16": "ceil_gather128",
                 "probe16_hbm": "ceil_gather128",
-                "tabpart": "ceil_stream16u", "winorder": "ceil_copy"}
+                "tabpart": "ceil_stream16u", "winorder": "ceil_copy", "hashwin16": "ceil_copy"}
 # bytes per lane the ceiling kernels read and write (include/shf_hash_batch_ceiling.h)
 CEIL_READ_PER_LANE = {"ceil_copy": 16, "ceil_copynt": 16, "ceil_read16": 256, "ceil_read16nt": 256, "ceil_read16w1": 256,
                       "ceil_gather128": 132,
@@ -325,8 +327,8 @@ def grid_threads(name, n):
         return ((n + 63) // 64 + 1) // 2 * 128  # k_span_pp: one 128-thread workgroup per two tiles
     if name == "tabpart":
         return n * 512                  # k_tab_split: one 512-thread workgroup per tab
-    if name == "winorder":
-        return (n + 4095) // 4096 * 256  # k_wo_scatter: one 256-thread workgroup per 4096-key chunk
+    if name in ("winorder", "hashwin16"):
+        return (n + 4095) // 4096 * 256  # k_wo_scatter (and k_fixed16_win): one 256-thread workgroup per 4096 keys
     return None
 
 
@@ -446,6 +448,8 @@ def make_workloads(args, dev, rank, world=1):
         wl.append(tab_workload(args, dev, seed_base))
     if "winorder" in only:
         wl.append(win_order_workload(args, dev, seed_base))
+    if "hashwin16" in only:
+        wl.append(hash_win_workload(args, dev, fixed16_pairs()))
     wl += ceiling_workloads(args, dev, only, bufs, fixed16_pairs)
     torch.cuda.synchronize()
     return sorted(wl, key=lambda w: ORDER.index(w.name) if w.name in ORDER else len(ORDER))
@@ -662,9 +666,60 @@ def win_order_workload(args, dev, seed_base):
               np.array_equal(start.cpu().numpy().view(np.uint32), want_s))
         return bool(ok), int(n)
 
-    return Workload("winorder", n, 16 + 4, [launch], "k_wo_hist + k_wo_scan + k_wo_scatter",
+    return Workload("winorder", n, 16 + 4, [launch], "k_wo_hist + k_wo_scan_rows + k_wo_scatter",
                     "%d 16-B hash records ordered by window (stable counting sort, 3 launches)" % n, verify,
                     grid_threads("winorder", n))
+
+
+def hash_win_workload(args, dev, pairs):
+    """Hash + window order in one call (shf_hash_batch_fixed_win_async, SURVEY.md
+    §8 f1 "alongside"): configs[1]'s 10M 16-B keys -> 16-B records + the window
+    order (perm, win_start), rotating over fixed16's batches with an order buffer
+    and workspace each. Algorithmic bytes per key: 16 key + 16 record + 4 perm."""
+    import ctypes
+
+    import torch
+
+    import sharedhashfile_amd as hb
+
+    n = args.keys16
+    lib = hb.load()
+    need = lib.shf_win_order_workspace_bytes(n)
+    fn = lib.shf_hash_batch_fixed_win_async
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    bufs, launches = [], []
+    for keys, out in pairs:
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        start = torch.empty(257, dtype=torch.int32, device=dev)
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        bufs.append((keys, out, perm, start, ws))
+        argv = (ctypes.c_void_p(keys.data_ptr()), ctypes.c_uint32(16), ctypes.c_uint64(n), ctypes.c_uint32(SEED),
+                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(perm.data_ptr()), ctypes.c_void_p(start.data_ptr()),
+                ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(need), st)
+
+        def launch(argv=argv):
+            rc = fn(*argv)
+            if rc:
+                raise hb.ShfHashBatchError(rc, "shf_hash_batch_fixed_win_async")
+
+        launches.append(launch)
+
+    def verify():
+        from oracle.oracle_py import Oracle
+
+        ok, checked = verify_fixed([(b[0], b[1]) for b in bufs], 16, VERIFY_SAMPLES, 17)
+        for keys, out, perm, start, _ in bufs[:1]:  # the whole order of one batch, from its own records
+            want_p, want_s = Oracle.win_order(out.cpu().numpy().view(np.uint64))
+            ok = ok and np.array_equal(perm.cpu().numpy().view(np.uint32), want_p) and \
+                np.array_equal(start.cpu().numpy().view(np.uint32), want_s)
+            checked += n
+        return bool(ok), int(checked)
+
+    w = Workload("hashwin16", n, 16 + 16 + 4, launches, "k_fixed16_win + k_wo_scan_rows + k_wo_scatter",
+                 "%d 16-B keys hashed and window-ordered in one call (records + perm), rotating over %d batches"
+                 % (n, len(pairs)), verify, grid_threads("hashwin16", n))
+    w.keep = bufs
+    return w
 
 
 def tab_workload(args, dev, seed_base):
@@ -997,7 +1052,7 @@ def pmc_child_sizes(args, want):
     child = argparse.Namespace(keys256=k256, keys16=args.keys16)
     sizes = {"fixed16": args.keys16, "fixed256": k256, "var": kvar, "probe16": args.keys16,
              "probe16_hbm": args.keys16 - 256,
-             "tabpart": args.tab_jobs, "winorder": args.keys16, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
+             "tabpart": args.tab_jobs, "winorder": args.keys16, "hashwin16": args.keys16, "ceil_copy": args.keys16, "ceil_copynt": args.keys16,
              "ceil_read16": read16_lanes(child, set(want)), "ceil_read16nt": read16_lanes(child, set(want)),
              "ceil_read16w1": read16_lanes(child, set(want)),
              "ceil_gather128": args.keys16, "ceil_stream16u": 2 * args.keys16, "ceil_valu_add": VALU_LANES,
@@ -1008,18 +1063,36 @@ def pmc_child_sizes(args, want):
 def parse_pmc_rows(rows, grids):
     """{workload: {counter: [values]}} from rocprofv3 counter_collection rows:
     a row counts for a workload when its kernel name holds the workload's
-    symbol and its grid is the workload's launch grid."""
+    symbol and its grid is the workload's launch grid. A kernel that several
+    multi-kernel workloads share (MULTI_KERNEL: the order passes) counts for the
+    workload whose own first kernel ran last before it (rows in dispatch order)."""
     vals = {}
-    for row in rows:
+    multi = [w for w in grids if w in MULTI_KERNEL]
+    owner_of = {}  # a multi-kernel workload's own kernels (those no other workload of the run has)
+    for w in multi:
+        for sym in MULTI_KERNEL[w]:
+            if sum(sym in MULTI_KERNEL[v] for v in multi) == 1:
+                owner_of[sym] = w
+
+    def order(r):
+        try:
+            return int(float(r.get("Dispatch_Id") or 0))
+        except ValueError:
+            return 0
+    current = None
+    for row in sorted(rows, key=order):
         name = row.get("Kernel_Name", "")
         try:
             grid = int(float(row.get("Grid_Size") or -1))
         except ValueError:
             grid = -1
+        own = next((w for sym, w in owner_of.items() if sym in name), None)
+        if own is not None:
+            current = own
         for w, g in grids.items():
             if w in MULTI_KERNEL:
                 for sym in MULTI_KERNEL[w]:
-                    if sym in name:
+                    if sym in name and (own == w or (own is None and (sym in owner_of or current == w))):
                         vals.setdefault(w, {}).setdefault((sym, row.get("Counter_Name")), []).append(
                             float(row["Counter_Value"]))
             elif KERNEL_SYMS[w] in name and (g is None or grid < 0 or grid == g):
@@ -1374,6 +1447,8 @@ def compact_line(full, detail_path):
             e["scaling"] = s["scaling"]
         if s.get("shards"):
             e["shards"] = s["shards"]
+        if name == "hashwin16" and ro.get("kernel_us"):
+            e["x_fixed16"] = round(r["kernel_us"] / ro["kernel_us"], 3)  # hash + order over the hash alone
         sec[name] = e
     line["secondary"] = sec
     line["ceilings_gbs"] = ceil

@@ -333,6 +333,35 @@ SHF_HB_API int shf_win_order_async(const shf_hash128 *d_hashes, uint64_t n, uint
                                    void *hip_stream);
 SHF_HB_API int shf_win_order(const shf_hash128 *hashes, uint64_t n, uint32_t *perm, uint32_t *win_start, int mem);
 
+/* ---- hash + window order in one call ("alongside") -------
+ *
+ * The 16-B records of shf_hash_batch_fixed_async / shf_hash_batch_var_async in
+ * d_out, and their window order in d_perm / d_win_start exactly as
+ * shf_win_order_async would compute it from d_out -- without reading d_out
+ * back: the hashing kernel writes each key's window byte beside its record
+ * into the workspace (for 16-B keys it also counts each 4096-key chunk's
+ * windows), and the order passes work from those bytes. d_workspace: at least
+ * shf_win_order_workspace_bytes(n) bytes, 16-B aligned. n < 2^32. Enqueued on
+ * hip_stream like the other _async calls; variable-length key errors are
+ * reported by shf_hash_batch_status() (an invalid key's record is not written
+ * and its window byte is then unspecified, so perm is too). */
+SHF_HB_API int shf_hash_batch_fixed_win_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                              shf_hash128 *d_out, uint32_t *d_perm, uint32_t *d_win_start,
+                                              void *d_workspace, size_t workspace_bytes, void *hip_stream);
+SHF_HB_API int shf_hash_batch_var_win_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                                            uint32_t seed, shf_hash128 *d_out, uint32_t *d_perm,
+                                            uint32_t *d_win_start, void *d_workspace, size_t workspace_bytes,
+                                            void *hip_stream);
+/* The same with a forced hashing kernel (tests and benchmarks; SHF_HB_KERNEL_*). */
+SHF_HB_API int shf_hash_batch_fixed_win_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n,
+                                                     uint32_t seed, shf_hash128 *d_out, uint32_t *d_perm,
+                                                     uint32_t *d_win_start, void *d_workspace,
+                                                     size_t workspace_bytes, int kernel, void *hip_stream);
+SHF_HB_API int shf_hash_batch_var_win_kernel_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                                                   uint32_t seed, shf_hash128 *d_out, uint32_t *d_perm,
+                                                   uint32_t *d_win_start, void *d_workspace,
+                                                   size_t workspace_bytes, int kernel, void *hip_stream);
+
 /* ---- status of asynchronous variable-length calls -------------------------
  * Waits for hip_stream (NULL = the null stream), then returns SHF_HB_ERR_ARG if
  * any asynchronous variable-length call (hashing, UID parts or probe) that

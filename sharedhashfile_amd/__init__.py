@@ -97,6 +97,11 @@ _SIGS = {
     "shf_win_order_workspace_bytes": [_U64],
     "shf_win_order_async": [_VP, _U64, _VP, _VP, _VP, ctypes.c_size_t, _VP],
     "shf_win_order": [_VP, _U64, _VP, _VP, _INT],
+    "shf_hash_batch_fixed_win_async": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP],
+    "shf_hash_batch_var_win_async": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP],
+    "shf_hash_batch_fixed_win_kernel_async": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _INT,
+                                              _VP],
+    "shf_hash_batch_var_win_kernel_async": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _INT, _VP],
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
@@ -485,6 +490,67 @@ def win_order(hashes, perm=None, win_start=None, workspace=None, stream=None):
         # caching allocator from handing its bytes out before that stream gets there
         workspace.record_stream(stream)
     return perm, win_start
+
+
+def _win_outputs(n, dev, out, perm, win_start, workspace):
+    import torch
+
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    _require_out(out, (n, 2), _offset_dtypes(), dev)
+    if perm is None:
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+    _require_out(perm, (n,), (torch.int32,), dev)
+    if win_start is None:
+        win_start = torch.empty(257, dtype=torch.int32, device=dev)
+    _require_out(win_start, (257,), (torch.int32,), dev)
+    own_ws = workspace is None
+    if own_ws:
+        workspace = torch.empty(max(load().shf_win_order_workspace_bytes(n), 1), dtype=torch.uint8, device=dev)
+    _require_cuda_u8(workspace, "workspace")
+    return out, perm, win_start, workspace, own_ws
+
+
+def hash_fixed_win(keys, key_len, seed=SEED, out=None, perm=None, win_start=None, workspace=None, stream=None,
+                   kernel=KERNEL_AUTO):
+    """Hash + window order in one call (shf_hash_batch_fixed_win_async):
+    returns (hashes (n, 2) int64, perm int32[n], win_start int32[257]), the
+    order exactly what win_order(hashes) gives, computed from the window bytes
+    the hashing kernel writes beside the records."""
+    _require_cuda_u8(keys, "keys")
+    if key_len <= 0 or keys.numel() % key_len:
+        raise ValueError("keys.numel() must be a multiple of key_len")
+    n = keys.numel() // key_len
+    out, perm, win_start, workspace, own_ws = _win_outputs(n, keys.device, out, perm, win_start, workspace)
+    with _on(keys):
+        rc = load().shf_hash_batch_fixed_win_kernel_async(
+            ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()),
+            ctypes.c_void_p(perm.data_ptr()), ctypes.c_void_p(win_start.data_ptr()),
+            ctypes.c_void_p(workspace.data_ptr()), workspace.numel(), kernel, _stream_handle(stream))
+    _check(rc, "shf_hash_batch_fixed_win_kernel_async")
+    if stream is not None and own_ws:
+        workspace.record_stream(stream)
+    return out, perm, win_start
+
+
+def hash_var_win(data, offsets, seed=SEED, out=None, perm=None, win_start=None, workspace=None, stream=None,
+                 kernel=KERNEL_AUTO):
+    """Variable-length keys: hash + window order in one call (shf_hash_batch_var_win_async)."""
+    _require_cuda_u8(data, "data")
+    _require_cuda(offsets, "offsets", _offset_dtypes())
+    n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets needs n + 1 entries")
+    out, perm, win_start, workspace, own_ws = _win_outputs(n, data.device, out, perm, win_start, workspace)
+    with _on(data):
+        rc = load().shf_hash_batch_var_win_kernel_async(
+            ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(perm.data_ptr()), ctypes.c_void_p(win_start.data_ptr()),
+            ctypes.c_void_p(workspace.data_ptr()), workspace.numel(), kernel, _stream_handle(stream))
+    _check(rc, "shf_hash_batch_var_win_kernel_async")
+    if stream is not None and own_ws:
+        workspace.record_stream(stream)
+    return out, perm, win_start
 
 
 def win_order_host(hashes):

@@ -10,8 +10,9 @@ namespace shfhb {
 
 // kOutHash: 16-B SHF_HASH records; kOutUid: 8-B packed UID parts;
 // kOutProbe: 16-B shf_probe records (row pre-probe), plus the
-// hashes when Sink::hash_out is set.
-enum OutMode { kOutHash = 0, kOutUid = 1, kOutProbe = 2 };
+// hashes when Sink::hash_out is set; kOutHashWin: the 16-B records plus each
+// key's window byte (h1 & 0xff, shf.c:800) for the window order (win_order.hip).
+enum OutMode { kOutHash = 0, kOutUid = 1, kOutProbe = 2, kOutHashWin = 3 };
 enum KernelChoice {
   kKernelAuto = 0,
   kKernelFixed16 = 1,
@@ -32,7 +33,26 @@ struct Sink {
   const uint8_t* map8 = nullptr;       // kOutProbe: compact copy of tab_slot (launch_compact_map), or null
   const uint32_t* win_tab = nullptr;
   uint32_t* status = nullptr;  // variable-length keys: set to 1 when a key's offsets are invalid
+  uint8_t* wins = nullptr;     // kOutHashWin: n window bytes (rounded up to whole kWoChunk chunks)
+  uint32_t* win_counts = nullptr;  // kOutHashWin, fused 16-B kernel: each chunk's 256-bin histogram
 };
+
+// Window-order geometry, shared by the hashing kernels' fused epilogue and the
+// order passes (win_order.hip): the batch is cut into chunks of kWoChunk keys;
+// each chunk has one row of kWoBins counts.
+constexpr uint32_t kWoChunk = 4096;
+constexpr uint32_t kWoBins = 256;  // SHF_WINS_PER_SHF
+// Counts are bin-major: bin b's row holds its count in chunk 0, 1, ... (the
+// scan turns it into the exclusive prefix, entry [chunks] = the bin's total),
+// rows kept 256-B aligned.
+__host__ __device__ inline uint64_t wo_row_stride(uint64_t chunks) { return (chunks + 1 + 63) & ~63ull; }
+// Workgroup g's chunk when the chunks are dealt XCD by XCD (workgroup g runs on
+// XCD g % 8): the workgroups of one XCD take consecutive chunks, so each 128-B
+// line of a counts row (32 consecutive chunks) is written through one L2.
+__device__ inline uint32_t xcd_major(uint32_t g, uint32_t groups) {
+  const uint32_t q = groups / 8u, r = groups % 8u, x = g % 8u;
+  return x * q + min(x, r) + g / 8u;
+}
 
 // keys: device pointer to n * key_len bytes.
 hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
@@ -70,5 +90,16 @@ hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint
 uint64_t win_order_workspace_bytes(uint64_t n);
 hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
                             hipStream_t st);
+// The workspace's window bytes and counts rows, for a hashing launch with
+// kOutHashWin to fill; then launch_win_order_bytes orders from them (counting
+// the chunks itself unless the hashing kernel did: hist_done).
+uint8_t* win_order_wins(void* workspace, uint64_t n);
+uint32_t* win_order_counts(void* workspace);
+hipError_t launch_win_order_bytes(uint64_t n, bool hist_done, uint32_t* perm, uint32_t* win_start, void* workspace,
+                                  hipStream_t st);
+// Fixed-length hash + window bytes (kOutHashWin): 16-B keys go through the fused
+// kernel, which also writes the chunk histograms (*hist_done = true).
+hipError_t launch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
+                            hipStream_t st, int kernel, bool* hist_done);
 
 }  // namespace shfhb

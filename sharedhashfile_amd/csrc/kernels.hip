@@ -183,9 +183,10 @@ __device__ __forceinline__ void store_probe(const Sink& sink, uint64_t i, const 
 
 template <int OUT>
 __device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const State& s) {
-  if constexpr (OUT == kOutHash) {
+  if constexpr (OUT == kOutHash || OUT == kOutHashWin) {
     const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + i);
+    if constexpr (OUT == kOutHashWin) sink.wins[i] = (uint8_t)s.h1;  // the window, shf.c:800
   } else if constexpr (OUT == kOutUid) {
     __builtin_nontemporal_store(uid_parts(s), reinterpret_cast<uint64_t*>(sink.out) + i);
   } else {
@@ -251,6 +252,48 @@ __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__
   body_block(s, pack64(k.x, k.y), pack64(k.z, k.w));
   finish(s, 16);
   store_result<OUT>(sink, i, s);
+}
+
+// 16-B keys hashed and counted for the window order in one pass (kOutHashWin):
+// one workgroup per kWoChunk-key chunk, kWoChunk / BLOCK keys per lane
+// (lane t takes keys BLOCK j + t, so each load instruction reads BLOCK x 16 B of
+// consecutive keys; all of them in flight before the first is hashed). Beside
+// each hash record it writes the key's window byte and the chunk's 256-bin
+// histogram (LDS atomics, into the bin-major counts): the order passes then
+// never read the 16-B records back (win_order.hip).
+template <uint32_t BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_fixed16_win(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
+                                                       Sink sink) {
+  constexpr uint32_t kKpl = kWoChunk / BLOCK;
+  __shared__ uint32_t hist[kWoBins];
+  __shared__ __attribute__((aligned(16))) uint8_t cwb[kWoChunk];
+  const uint32_t t = threadIdx.x;
+  const uint32_t c = sink.n_slots ? blockIdx.x : xcd_major(blockIdx.x, gridDim.x);  // EXPERIMENT: n_slots = plain map
+  const uint64_t k0 = (uint64_t)c * kWoChunk;
+  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
+  if (t < kWoBins) hist[t] = 0;
+  u32x4 k[kKpl];  // past the batch: the last key again (hashed, neither stored nor counted)
+#pragma unroll
+  for (uint32_t j = 0; j < kKpl; ++j) k[j] = __builtin_nontemporal_load(&keys[k0 + min(BLOCK * j + t, kn - 1u)]);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kKpl; ++j) {
+    const uint32_t i = BLOCK * j + t;
+    State s{seed, seed};
+    body_block(s, pack64(k[j].x, k[j].y), pack64(k[j].z, k[j].w));
+    finish(s, 16);
+    const uint32_t w = (uint32_t)s.h1 & 0xffu;
+    if (i < kn) {
+      const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + k0 + i);
+      atomicAdd(&hist[w], 1u);
+    }
+    cwb[i] = (uint8_t)w;
+  }
+  __syncthreads();
+  if (t < kWoBins) sink.win_counts[(uint64_t)t * wo_row_stride(gridDim.x) + c] = hist[t];
+  // the chunk's window bytes, 16 per thread (the workspace holds whole chunks)
+  if (t < kWoChunk / 16u) reinterpret_cast<u32x4*>(sink.wins + k0)[t] = reinterpret_cast<const u32x4*>(cwb)[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -1233,9 +1276,36 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
       return launch_fixed_t<kOutHash>(keys, key_len, n, seed, sink, st, kernel);
     case kOutUid:
       return launch_fixed_t<kOutUid>(keys, key_len, n, seed, sink, st, kernel);
+    case kOutHashWin: {
+      bool hist_done = false;
+      return launch_fixed_win(keys, key_len, n, seed, sink, st, kernel, &hist_done);
+    }
     default:
       return launch_fixed_t<kOutProbe>(keys, key_len, n, seed, sink, st, kernel);
   }
+}
+
+hipError_t launch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
+                            hipStream_t st, int kernel, bool* hist_done) {
+  *hist_done = false;
+  if (n == 0) return hipSuccess;
+  const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
+  if (key_len == 16 && al16 && sink.win_counts && (kernel == kKernelAuto || kernel == kKernelFixed16)) {
+    const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
+    if (chunks > 0x7fffffffull) return hipErrorInvalidValue;
+    const char* e = getenv("SHF_HB_F16WIN_BLOCK");  // EXPERIMENT (removed once a shape is chosen)
+    const int blk = e ? atoi(e) : 256;
+    const char* pm = getenv("SHF_HB_F16WIN_PLAIN");
+    Sink sk = sink;
+    sk.n_slots = pm && pm[0] == '1';
+    const u32x4* k4 = reinterpret_cast<const u32x4*>(keys);
+    if (blk == 1024) hipLaunchKernelGGL(k_fixed16_win<1024>, dim3((unsigned)chunks), dim3(1024), 0, st, k4, n, seed, sk);
+    else if (blk == 512) hipLaunchKernelGGL(k_fixed16_win<512>, dim3((unsigned)chunks), dim3(512), 0, st, k4, n, seed, sk);
+    else hipLaunchKernelGGL(k_fixed16_win<256>, dim3((unsigned)chunks), dim3(256), 0, st, k4, n, seed, sk);
+    *hist_done = true;
+    return hipGetLastError();
+  }
+  return launch_fixed_t<kOutHashWin>(keys, key_len, n, seed, sink, st, kernel);
 }
 
 hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_base, uint64_t n, uint32_t seed,
@@ -1246,6 +1316,8 @@ hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_b
       return launch_var_t<kOutHash>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     case kOutUid:
       return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
+    case kOutHashWin:
+      return launch_var_t<kOutHashWin>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     default:
       return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
   }

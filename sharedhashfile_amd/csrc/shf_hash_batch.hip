@@ -860,6 +860,12 @@ bool fixed_kernel_fits(const void* d_keys, uint32_t key_len, int kernel) {
 }
 
 
+// A caller's window-order workspace: big enough for n keys and 16-B aligned
+// (the window bytes move 16 B at a time).
+bool win_workspace_ok(const void* ws, size_t bytes, uint64_t n) {
+  return ws && bytes >= shfhb::win_order_workspace_bytes(n) && ((uintptr_t)ws & 15u) == 0;
+}
+
 // Probe sink for `index` on the calling thread's current device.
 int probe_sink(const shf_row_index* index, void* d_probe, void* d_hashes, shfhb::Sink* sink) {
   if (!index || !d_probe) return SHF_HB_ERR_ARG;
@@ -1018,6 +1024,63 @@ int shf_uid_parts_batch_var_async(const void* d_bytes, const uint64_t* d_offsets
   if (n == 0) return SHF_HB_OK;
   if (!d_parts || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_parts), shfhb::kOutUid, (hipStream_t)hip_stream, false);
+}
+
+int shf_hash_batch_fixed_win_kernel_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                          shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start,
+                                          void* d_workspace, size_t workspace_bytes, int kernel, void* hip_stream) {
+  if (n == 0 && !d_win_start) return SHF_HB_OK;
+  if (n && (!d_out || !d_perm || (!d_keys && key_len))) return SHF_HB_ERR_ARG;
+  if (key_len > kMaxKeyLen || n > 0xffffffffull || !fixed_kernel_fits(d_keys, key_len, kernel)) return SHF_HB_ERR_ARG;
+  if (n && !win_workspace_ok(d_workspace, workspace_bytes, n)) return SHF_HB_ERR_ARG;
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  const hipStream_t st = (hipStream_t)hip_stream;
+  bool hist_done = false;
+  if (n) {
+    shfhb::Sink k = out_sink(d_out);
+    k.wins = shfhb::win_order_wins(d_workspace, n);
+    k.win_counts = shfhb::win_order_counts(d_workspace);
+    HB_TRY(shfhb::launch_fixed_win(d_keys, key_len, n, seed, k, st, kernel, &hist_done));
+  }
+  HB_TRY(shfhb::launch_win_order_bytes(n, hist_done, d_perm, d_win_start, d_workspace, st));
+  return SHF_HB_OK;
+}
+
+int shf_hash_batch_fixed_win_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                   shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start, void* d_workspace,
+                                   size_t workspace_bytes, void* hip_stream) {
+  return shf_hash_batch_fixed_win_kernel_async(d_keys, key_len, n, seed, d_out, d_perm, d_win_start, d_workspace,
+                                                workspace_bytes, SHF_HB_KERNEL_AUTO, hip_stream);
+}
+
+int shf_hash_batch_var_win_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
+                                        shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start,
+                                        void* d_workspace, size_t workspace_bytes, int kernel, void* hip_stream) {
+  if (n == 0 && !d_win_start) return SHF_HB_OK;
+  if (n && (!d_out || !d_perm || !d_offsets || !d_bytes)) return SHF_HB_ERR_ARG;
+  if (n > 0xffffffffull || !var_kernel_valid(kernel)) return SHF_HB_ERR_ARG;
+  if (n && !win_workspace_ok(d_workspace, workspace_bytes, n)) return SHF_HB_ERR_ARG;
+  shfhb::Sink k = out_sink(d_out);
+  if (n) {
+    k.wins = shfhb::win_order_wins(d_workspace, n);
+    int rc = device_var(d_bytes, d_offsets, n, seed, k, shfhb::kOutHashWin, (hipStream_t)hip_stream, false, kernel);
+    if (rc) return rc;
+  } else {
+    DevCtx* c = nullptr;
+    int rc = current_ctx(&c);
+    if (rc) return rc;
+  }
+  HB_TRY(shfhb::launch_win_order_bytes(n, false, d_perm, d_win_start, d_workspace, (hipStream_t)hip_stream));
+  return SHF_HB_OK;
+}
+
+int shf_hash_batch_var_win_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
+                                 shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start, void* d_workspace,
+                                 size_t workspace_bytes, void* hip_stream) {
+  return shf_hash_batch_var_win_kernel_async(d_bytes, d_offsets, n, seed, d_out, d_perm, d_win_start, d_workspace,
+                                             workspace_bytes, SHF_HB_KERNEL_AUTO, hip_stream);
 }
 
 int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
@@ -1246,9 +1309,7 @@ int shf_win_order_async(const shf_hash128* d_hashes, uint64_t n, uint32_t* d_per
                         void* d_workspace, size_t workspace_bytes, void* hip_stream) {
   if (n == 0 && !d_win_start) return SHF_HB_OK;
   if (n > 0xffffffffull) return SHF_HB_ERR_ARG;
-  if (n && (!d_hashes || !d_perm || !d_workspace || workspace_bytes < shfhb::win_order_workspace_bytes(n)))
-    return SHF_HB_ERR_ARG;
-  if (((uintptr_t)d_workspace & 15u) != 0) return SHF_HB_ERR_ARG;  // the window bytes move 16 B at a time
+  if (n && (!d_hashes || !d_perm || !win_workspace_ok(d_workspace, workspace_bytes, n))) return SHF_HB_ERR_ARG;
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;

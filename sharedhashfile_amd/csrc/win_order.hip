@@ -25,6 +25,7 @@
 // written through the same L2 and leave HBM as whole lines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/shf_hash_batch.h"
 #include "kernels.h"
@@ -34,18 +35,11 @@ namespace shfhb {
 namespace {
 
 constexpr uint32_t kWoThreads = 256;                 // 4 waves
-constexpr uint32_t kWoSub = 1024;                    // keys per wave (16 steps of 64) in the scatter
-constexpr uint32_t kWoChunk = 4 * kWoSub;            // keys per workgroup (a chunk)
-constexpr uint32_t kWoBins = 256;                    // SHF_WINS_PER_SHF
+constexpr uint32_t kWoSub = kWoChunk / 4;            // keys per wave (16 steps of 64) in the scatter
+static_assert(kWoChunk == 4096 && kWoBins == 256, "one chunk = 4 waves x 16 steps x 64 keys; one bin per thread");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Workgroup g's place in XCD-major order: the g % 8 == x workgroups of a launch
-// (those on XCD x) take consecutive slots.
-__device__ __forceinline__ uint32_t xcd_major(uint32_t g, uint32_t groups) {
-  const uint32_t q = groups / 8u, r = groups % 8u, x = g % 8u;
-  return x * q + min(x, r) + g / 8u;
-}
 
 __device__ __forceinline__ uint32_t win_of(const u32x4* hashes, uint64_t key) {
   return __builtin_nontemporal_load(&hashes[key]).x & 0xffu;  // h1's low byte (shf.c:800)
@@ -57,7 +51,7 @@ __device__ __forceinline__ uint32_t win_of(const u32x4* hashes, uint64_t key) {
 // consecutive records); the window bytes gather in LDS and leave as 16 B per
 // thread.
 __global__ __launch_bounds__(kWoThreads) void k_wo_hist(const u32x4* __restrict__ hashes, uint64_t n,
-                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ wins) {
+                                                       uint32_t* __restrict__ counts, uint8_t* __restrict__ wins) {
   __shared__ uint32_t hist[kWoBins];
   __shared__ uint8_t cwb[kWoChunk];
   const uint32_t t = threadIdx.x;
@@ -78,54 +72,89 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_hist(const u32x4* __restrict_
     cwb[i] = (uint8_t)w[st];
   }
   __syncthreads();
-  counts[(uint64_t)c * kWoBins + t] = hist[t];
+  counts[(uint64_t)t * wo_row_stride(gridDim.x) + c] = hist[t];
   // 16 window bytes per thread (bytes past the batch land in the workspace's last chunk, unused)
-  reinterpret_cast<u32x4*>(wins + (k0 >> 2))[t] = reinterpret_cast<const u32x4*>(cwb)[t];
+  reinterpret_cast<u32x4*>(wins + k0)[t] = reinterpret_cast<const u32x4*>(cwb)[t];
 }
 
-// The chunks' counts scanned per bin in two levels, rows read whole (a row =
-// one chunk's 256 counts, 1 KiB; thread t = bin t):
-//   k_wo_scan_blocks  one workgroup per block of kWoScanBlock chunks: exclusive
-//                     prefix of each bin over the block's rows, in place, and
-//                     the block's sums (bsum[block][bin]);
-//   k_wo_scan_top     one workgroup: exclusive prefix of each bin over the
-//                     blocks' sums, in place, and the bins' totals.
-// A chunk's prefix is then counts[c][bin] + bsum[c / kWoScanBlock][bin].
-// (One workgroup per bin reading its column, 4-B words 1 KiB apart: 13.4 us
-// per 10M keys.)
-constexpr uint32_t kWoScanBlock = 64;
-__global__ __launch_bounds__(256) void k_wo_scan_blocks(uint32_t* __restrict__ counts, uint32_t chunks,
-                                                        uint32_t* __restrict__ bsum) {
-  const uint32_t t = threadIdx.x, c0 = blockIdx.x * kWoScanBlock;
-  uint32_t v[kWoScanBlock];
+// The same histogram from the window bytes a hashing kernel wrote beside its
+// records (kOutHashWin): 1 B per key read instead of the 16-B record. Thread t
+// takes the chunk's bytes [16 t, 16 t + 16) (one 16-B load; the workspace holds
+// whole chunks, bytes past the batch are not counted).
+__global__ __launch_bounds__(kWoThreads) void k_wo_hist_bytes(const uint8_t* __restrict__ wins, uint64_t n,
+                                                             uint32_t* __restrict__ counts) {
+  __shared__ uint32_t hist[kWoBins];
+  const uint32_t t = threadIdx.x, c = xcd_major(blockIdx.x, gridDim.x);
+  hist[t] = 0;
+  const uint64_t k0 = (uint64_t)c * kWoChunk;
+  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wins + k0) + t);
+  __syncthreads();
+  const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (uint32_t r = 0; r < kWoScanBlock; ++r)  // every load in flight first (past the end: the last row, unused)
-    v[r] = counts[(uint64_t)min(c0 + r, chunks - 1u) * kWoBins + t];
-  uint32_t run = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < kWoScanBlock; ++r) {
-    if (c0 + r < chunks) counts[(uint64_t)(c0 + r) * kWoBins + t] = run;
-    run += c0 + r < chunks ? v[r] : 0u;
-  }
-  bsum[(uint64_t)blockIdx.x * kWoBins + t] = run;
+  for (uint32_t q = 0; q < 16u; ++q)
+    if (16u * t + q < kn) atomicAdd(&hist[(w4[q >> 2] >> (8u * (q & 3u))) & 0xffu], 1u);
+  __syncthreads();
+  counts[(uint64_t)t * wo_row_stride(gridDim.x) + c] = hist[t];
 }
 
-__global__ __launch_bounds__(256) void k_wo_scan_top(uint32_t* __restrict__ bsum, uint32_t blocks,
-                                                     uint32_t* __restrict__ totals) {
-  constexpr uint32_t kBatch = 16;
-  const uint32_t t = threadIdx.x;
-  uint32_t run = 0;
-  for (uint32_t b0 = 0; b0 < blocks; b0 += kBatch) {
-    uint32_t v[kBatch];
+// The chunks' counts scanned per bin in one launch: one workgroup per bin
+// scans its row (bin-major counts: the row is contiguous), 16 consecutive
+// chunks per thread (four 16-B loads) and 4096 per pass, and writes the
+// exclusive prefix back in place, then the bin's total at entry [chunks].
+__global__ __launch_bounds__(256) void k_wo_scan_rows(uint32_t* __restrict__ counts, uint32_t chunks) {
+  constexpr uint32_t kPer = 16;
+  __shared__ uint32_t wsum[4];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  uint32_t* row = counts + (uint64_t)blockIdx.x * wo_row_stride(chunks);
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < chunks; c0 += 256u * kPer) {
+    const uint32_t cb = c0 + kPer * t;  // this thread's first chunk (16-B aligned: c0 and kPer are)
+    uint32_t v[kPer];
 #pragma unroll
-    for (uint32_t r = 0; r < kBatch; ++r) v[r] = bsum[(uint64_t)min(b0 + r, blocks - 1u) * kWoBins + t];
-#pragma unroll
-    for (uint32_t r = 0; r < kBatch; ++r) {
-      if (b0 + r < blocks) bsum[(uint64_t)(b0 + r) * kWoBins + t] = run;
-      run += b0 + r < blocks ? v[r] : 0u;
+    for (uint32_t q = 0; q < kPer / 4; ++q) {
+      const u32x4 x = cb + 4u * q < chunks ? *reinterpret_cast<const u32x4*>(row + cb + 4u * q) : u32x4{0, 0, 0, 0};
+      v[4 * q] = x.x, v[4 * q + 1] = x.y, v[4 * q + 2] = x.z, v[4 * q + 3] = x.w;
     }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j)
+      if (cb + j >= chunks) v[j] = 0;  // a 16-B load may reach past the last chunk (the row's slack)
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) sum += v[j];
+    uint32_t inc = sum;  // inclusive scan of the threads' sums over the wave
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)inc, d);
+      if (lane >= d) inc += u;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t run = carry + inc - sum, block = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) {
+      run += w < wave ? wsum[w] : 0u;
+      block += wsum[w];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPer / 4; ++q) {
+      u32x4 x;
+      x.x = run, run += v[4 * q];
+      x.y = run, run += v[4 * q + 1];
+      x.z = run, run += v[4 * q + 2];
+      x.w = run, run += v[4 * q + 3];
+      if (cb + 4u * q + 3u < chunks) {
+        *reinterpret_cast<u32x4*>(row + cb + 4u * q) = x;
+      } else {
+        if (cb + 4u * q < chunks) row[cb + 4u * q] = x.x;
+        if (cb + 4u * q + 1u < chunks) row[cb + 4u * q + 1u] = x.y;
+        if (cb + 4u * q + 2u < chunks) row[cb + 4u * q + 2u] = x.z;
+      }
+    }
+    carry += block;
+    __syncthreads();  // wsum is rewritten by the next pass
   }
-  totals[t] = run;
+  if (t == 0) row[chunks] = carry;
 }
 
 // One chunk per workgroup, in two phases. (1) The chunk's stable order in LDS:
@@ -146,9 +175,7 @@ __global__ __launch_bounds__(256) void k_wo_scan_top(uint32_t* __restrict__ bsum
 // A wave's LDS accesses execute in order, and the compiler keeps the order of
 // these aliasing ones: no fence between steps.
 __global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __restrict__ wins, uint64_t n,
-                                                          uint32_t chunks, const uint32_t* __restrict__ counts,
-                                                          const uint32_t* __restrict__ bsum,
-                                                          const uint32_t* __restrict__ totals,
+                                                          const uint32_t* __restrict__ counts,
                                                           uint32_t* __restrict__ perm,
                                                           uint32_t* __restrict__ win_start) {
   __shared__ uint32_t next[4][kWoBins];         // per wave: the window's next local position
@@ -164,8 +191,9 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __rest
   // every global load first: the chunk's 4 KiB of window bytes (16 B per thread;
   // the workspace holds whole chunks), window t's total and this chunk's prefix
   const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
-  const uint32_t tot = totals[t];
-  const uint32_t pre = counts[(uint64_t)c * kWoBins + t] + bsum[(uint64_t)(c / kWoScanBlock) * kWoBins + t];
+  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
+  const uint32_t tot = row[gridDim.x];  // window t's keys in the batch (k_wo_scan_rows)
+  const uint32_t pre = row[c];          // ... in the chunks before this one
   cw[4u * t + 0] = cwv.x;
   cw[4u * t + 1] = cwv.y;
   cw[4u * t + 2] = cwv.z;
@@ -259,34 +287,176 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __rest
   }
 }
 
-}  // namespace
-
-uint64_t win_order_workspace_bytes(uint64_t n) {  // counts, totals, then the window bytes (whole chunks)
-  const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
-  const uint64_t blocks = (chunks + kWoScanBlock - 1) / kWoScanBlock;
-  return ((chunks + blocks) * kWoBins + kWoBins) * sizeof(uint32_t) + chunks * kWoChunk;
+// The lanes of the wave whose window byte equals this lane's (its "peers",
+// itself included): eight ballots, one per bit of the byte, each folded into
+// the lanes that differ from this one in that bit (v_bitop3: diff |= m ^ bal).
+__device__ __forceinline__ uint64_t match_byte(uint32_t w) {
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)w, b, 1);  // 0 or ~0: this lane's bit b
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(m != 0u);
+    lo = __builtin_amdgcn_bitop3_b32(lo, m, (uint32_t)bal, 0xF6);          // lo | (m ^ bal)
+    hi = __builtin_amdgcn_bitop3_b32(hi, m, (uint32_t)(bal >> 32), 0xF6);
+  }
+  return ~(((uint64_t)hi << 32) | lo);
 }
 
-hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
-                            hipStream_t st) {
+// k_wo_scatter with the step's peers found by ballots instead of LDS atomics:
+// (1) each wave walks its 1024 keys, 64 per step: a lane's rank among the
+// wave's keys of its window = the window's count so far (cnt, read) + its rank
+// among the step's peers; the lowest peer advances the count (one plain read and
+// one plain write per step, no atomics); (2) per window the waves' counts become
+// their first local positions; (3) each key goes to sorted[first + rank];
+// (4) out in order, as k_wo_scatter.
+__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t* __restrict__ wins, uint64_t n,
+                                                                 const uint32_t* __restrict__ counts,
+                                                                 uint32_t* __restrict__ perm,
+                                                                 uint32_t* __restrict__ win_start, uint32_t dbg) {
+  __shared__ uint32_t cnt[4][kWoBins];   // per wave: the window's keys so far, then its first local position
+  __shared__ uint32_t cw[kWoChunk / 4];  // the chunk's window bytes
+  __shared__ uint32_t sorted[kWoChunk];  // the chunk's keys in window order: offset | window << 16
+  __shared__ uint32_t gdelta[kWoBins];   // window t's perm position minus its local one
+  __shared__ uint32_t tsum[2][4];
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
+  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
+  const uint64_t k0 = (uint64_t)c * kWoChunk;
+  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
+  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
+  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
+  const uint32_t tot = row[gridDim.x];
+  const uint32_t pre = row[c];
+  cw[4u * t + 0] = cwv.x;
+  cw[4u * t + 1] = cwv.y;
+  cw[4u * t + 2] = cwv.z;
+  cw[4u * t + 3] = cwv.w;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
+  __syncthreads();
+  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
+  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
+  uint32_t ws[kWoSub / 64], rk[kWoSub / 64] = {};
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
+  // (1) ranks within the wave
+  if (!(dbg & 1))
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+    const bool valid = s0 + 64u * st + lane < s1;
+    const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+    const uint32_t base = cnt[wave][ws[st]];
+    rk[st] = base + rank;
+    if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // (2) window t: its keys in the chunk and in waves 0..v-1; exclusive scans over
+  // the windows of the totals (its base in perm) and of the chunk counts (its local start)
+  uint32_t hv[4], hc = 0;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    hv[v] = cnt[v][t];
+    hc += hv[v];
+  }
+  uint32_t it = tot, ih = hc;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
+    if (lane >= d) {
+      it += ut;
+      ih += uh;
+    }
+  }
+  if (lane == 63) {
+    tsum[0][wave] = it;
+    tsum[1][wave] = ih;
+  }
+  __syncthreads();
+  uint32_t bbase = it - tot, lbase = ih - hc;
+  for (uint32_t v = 0; v < wave; ++v) {
+    bbase += tsum[0][v];
+    lbase += tsum[1][v];
+  }
+  if (c == 0 && win_start) {
+    win_start[t] = bbase;
+    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
+  }
+  gdelta[t] = bbase + pre - lbase;
+  {
+    uint32_t run = lbase;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      cnt[v][t] = run;
+      run += hv[v];
+    }
+  }
+  __syncthreads();
+  // (3) the chunk's stable window order, in LDS
+  if (!(dbg & 2))
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+    const uint32_t i = s0 + 64u * st + lane;
+    if (i < s1) sorted[(cnt[wave][ws[st]] + rk[st]) & 4095u] = i | (ws[st] << 16);
+  }
+  __syncthreads();
+  // (4) out in that order: local position j holds key offset i of window w
+  uint32_t e[kWoChunk / kWoThreads];
+#pragma unroll
+  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) e[q] = sorted[min(t + kWoThreads * q, kn - 1u)];
+#pragma unroll
+  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
+    const uint32_t j = t + kWoThreads * q;
+    const uint32_t g = (dbg & 4) ? (uint32_t)k0 + j : min(gdelta[(e[q] >> 16) & 255u] + j, (uint32_t)n - 1u);
+    if (j < kn) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
+  }
+}
+
+}  // namespace
+
+// Workspace: the counts (bin-major rows, wo_row_stride), then the window bytes
+// (whole chunks; 16-B aligned: the rows are whole multiples of 256 B).
+uint64_t win_order_workspace_bytes(uint64_t n) {
+  const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
+  return kWoBins * wo_row_stride(chunks) * sizeof(uint32_t) + chunks * kWoChunk;
+}
+
+uint32_t* win_order_counts(void* workspace) { return static_cast<uint32_t*>(workspace); }
+
+uint8_t* win_order_wins(void* workspace, uint64_t n) {
+  const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
+  return reinterpret_cast<uint8_t*>(win_order_counts(workspace) + kWoBins * wo_row_stride(chunks));
+}
+
+// The scan and the scatter over counts and window bytes already in the
+// workspace (hist_done), or after counting the window bytes.
+hipError_t launch_win_order_bytes(uint64_t n, bool hist_done, uint32_t* perm, uint32_t* win_start, void* workspace,
+                                  hipStream_t st) {
   if (n == 0) {
     if (win_start) return hipMemsetAsync(win_start, 0, (kWoBins + 1) * sizeof(uint32_t), st);
     return hipSuccess;
   }
   if (n > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit key indices
   const uint32_t chunks = (uint32_t)((n + kWoChunk - 1) / kWoChunk);
-  const uint32_t blocks = (chunks + kWoScanBlock - 1) / kWoScanBlock;
-  uint32_t* counts = static_cast<uint32_t*>(workspace);
-  uint32_t* bsum = counts + (uint64_t)chunks * kWoBins;
-  uint32_t* totals = bsum + (uint64_t)blocks * kWoBins;
-  uint32_t* wins = totals + kWoBins;  // 16-B aligned: whole rows of 256 u32 before it
-  const u32x4* h = static_cast<const u32x4*>(hashes);
-  hipLaunchKernelGGL(k_wo_hist, dim3(chunks), dim3(kWoThreads), 0, st, h, n, counts, wins);
-  hipLaunchKernelGGL(k_wo_scan_blocks, dim3(blocks), dim3(256), 0, st, counts, chunks, bsum);
-  hipLaunchKernelGGL(k_wo_scan_top, dim3(1), dim3(256), 0, st, bsum, blocks, totals);
-  hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, reinterpret_cast<const uint8_t*>(wins), n,
-                     chunks, counts, bsum, totals, perm, win_start);
+  uint32_t* counts = win_order_counts(workspace);
+  const uint8_t* wins = win_order_wins(workspace, n);
+  if (!hist_done) hipLaunchKernelGGL(k_wo_hist_bytes, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts);
+  hipLaunchKernelGGL(k_wo_scan_rows, dim3(kWoBins), dim3(256), 0, st, counts, chunks);
+  const char* e = getenv("SHF_HB_WO_SCATTER");  // EXPERIMENT (removed once a variant is chosen)
+  if (e && e[0] == '2')
+    hipLaunchKernelGGL(k_wo_scatter_ballot, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start,
+                       (uint32_t)atoi(e + 1));
+  else
+    hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
   return hipGetLastError();
+}
+
+hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
+                            hipStream_t st) {
+  if (n == 0 || n > 0xffffffffull) return launch_win_order_bytes(n, true, perm, win_start, workspace, st);
+  const uint32_t chunks = (uint32_t)((n + kWoChunk - 1) / kWoChunk);
+  hipLaunchKernelGGL(k_wo_hist, dim3(chunks), dim3(kWoThreads), 0, st, static_cast<const u32x4*>(hashes), n,
+                     win_order_counts(workspace), win_order_wins(workspace, n));
+  return launch_win_order_bytes(n, true, perm, win_start, workspace, st);
 }
 
 }  // namespace shfhb

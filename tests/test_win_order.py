@@ -242,3 +242,113 @@ def test_window_disjoint_workers_put_and_find_every_key(oracle):
         with tempfile.TemporaryDirectory(dir=SHM) as d:
             found, _, _ = reference_put_get_procs(data, off, h, order, np.array(starts, np.uint64), d, "w", 1)
         assert found == n
+
+
+# ---------------------------------------------------------------------------
+# hash + window order in one call (shf_hash_batch_*_win_async): the records
+# bit-exact against the oracle, the order exactly the oracle's order of them
+# ---------------------------------------------------------------------------
+def _check_fused(out, perm, start, want_h):
+    import torch
+
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), want_h)
+    ref_perm, ref_start = Oracle.win_order(want_h)
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), ref_perm)
+    np.testing.assert_array_equal(start.cpu().numpy().view(np.uint32), ref_start)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 4095, 4096, 4097, 3 * 4096 + 77, 100_003, 1_000_001])
+@pytest.mark.parametrize("kernel", ["auto", "fixed16", "generic"])
+def test_fused_fixed16_hash_and_order(hb, dev, oracle, n, kernel):
+    """16-B keys: AUTO and FIXED16 run the fused kernel (k_fixed16_win: records,
+    window bytes and chunk histograms in one pass); GENERIC the per-key epilogue
+    (window bytes only, the chunks counted after)."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 256, size=n * 16, dtype=np.uint8)
+    k = {"auto": hb.KERNEL_AUTO, "fixed16": hb.KERNEL_FIXED16, "generic": hb.KERNEL_GENERIC}[kernel]
+    out, perm, start = hb.hash_fixed_win(torch.from_numpy(keys).to(dev), 16, kernel=k)
+    _check_fused(out, perm, start, oracle.hash_fixed(keys, 16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_len,kernel", [(256, "auto"), (256, "tiled"), (37, "auto"), (100, "span"), (8, "auto")])
+def test_fused_fixed_other_lengths(hb, dev, oracle, key_len, kernel):
+    import torch
+
+    n = 2 * 4096 + 321
+    rng = np.random.default_rng(key_len)
+    keys = rng.integers(0, 256, size=n * key_len, dtype=np.uint8)
+    k = {"auto": hb.KERNEL_AUTO, "tiled": hb.KERNEL_TILED, "span": hb.KERNEL_SPAN}[kernel]
+    out, perm, start = hb.hash_fixed_win(torch.from_numpy(keys).to(dev), key_len, kernel=k)
+    _check_fused(out, perm, start, oracle.hash_fixed(keys, key_len))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["auto", "span", "span_pp", "round", "generic"])
+def test_fused_var_hash_and_order(hb, dev, oracle, kernel):
+    import torch
+
+    data, off = _unique_keys(50_000, 21, 0, 512)
+    k = {"auto": hb.KERNEL_AUTO, "span": hb.KERNEL_SPAN, "span_pp": hb.KERNEL_SPAN_PP, "round": hb.KERNEL_ROUND,
+         "generic": hb.KERNEL_GENERIC}[kernel]
+    out, perm, start = hb.hash_var_win(torch.from_numpy(data).to(dev), torch.from_numpy(off.view(np.int64)).to(dev),
+                                       kernel=k)
+    _check_fused(out, perm, start, oracle.hash_var(data, off))
+
+
+@pytest.mark.gpu
+def test_fused_order_at_config_b_size(hb, dev, oracle):
+    """10M x 16-B keys (BASELINE configs[1]): the fused order equals the order of
+    the library's own records (size-independent property), sampled records
+    bit-exact against the oracle."""
+    import torch
+
+    from sharedhashfile_amd.keygen import device_random_bytes
+
+    n = 10_000_000
+    keys = device_random_bytes(n * 16, 77, dev)
+    out, perm, start = hb.hash_fixed_win(keys, 16)
+    p2, s2 = hb.win_order(out)
+    torch.cuda.synchronize()
+    assert torch.equal(perm, p2) and torch.equal(start, s2)
+    idx = np.random.default_rng(1).integers(0, n, size=20000)
+    ti = torch.from_numpy(idx).to(dev)
+    got = out.index_select(0, ti).cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got, oracle.hash_fixed(keys.view(n, 16).index_select(0, ti).cpu().numpy(), 16))
+    w = (out[:, 0] & 0xFF).to(torch.int64)
+    assert torch.equal(torch.bincount(w, minlength=256).cpu(), (s2[1:] - s2[:-1]).to(torch.int64).cpu())
+
+
+@pytest.mark.gpu
+def test_fused_rejects_bad_arguments(hb, dev):
+    import ctypes
+
+    import torch
+
+    lib = hb.load()
+    n = 5000
+    keys = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    p = torch.empty(n, dtype=torch.int32, device=dev)
+    need = lib.shf_win_order_workspace_bytes(n)
+    ws = torch.empty(need + 16, dtype=torch.uint8, device=dev)
+    vp = lambda t, d=0: ctypes.c_void_p(t.data_ptr() + d)
+    with torch.cuda.device(dev):
+        f = lib.shf_hash_batch_fixed_win_async
+        assert f(vp(keys), 16, n, 12345, vp(out), vp(p), None, vp(ws), need - 1, None) == hb.ERR_ARG
+        assert f(vp(keys), 16, n, 12345, vp(out), vp(p), None, vp(ws, 8), need, None) == hb.ERR_ARG
+        assert f(vp(keys), 16, n, 12345, None, vp(p), None, vp(ws), need, None) == hb.ERR_ARG
+        assert f(vp(keys), 16, 1 << 32, 12345, vp(out), vp(p), None, vp(ws), need, None) == hb.ERR_ARG
+        assert lib.shf_hash_batch_fixed_win_kernel_async(vp(keys), 16, n, 12345, vp(out), vp(p), None, vp(ws), need,
+                                                         hb.KERNEL_TILED, None) == hb.ERR_ARG
+        assert lib.shf_hash_batch_var_win_kernel_async(vp(keys), vp(keys), n, 12345, vp(out), vp(p), None, vp(ws),
+                                                       need, hb.KERNEL_TILED, None) == hb.ERR_ARG
+        s = torch.zeros(257, dtype=torch.int32, device=dev) + 5
+        assert f(None, 16, 0, 12345, None, None, vp(s), None, 0, None) == hb.OK  # empty batch: zeros
+        assert f(vp(keys), 16, n, 12345, vp(out), vp(p), None, vp(ws), need, None) == hb.OK
+    torch.cuda.synchronize(dev)
+    assert (s == 0).all()
