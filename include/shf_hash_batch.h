@@ -352,6 +352,18 @@ SHF_HB_API int shf_hash_batch_var_win_async(const void *d_bytes, const uint64_t 
                                             uint32_t seed, shf_hash128 *d_out, uint32_t *d_perm,
                                             uint32_t *d_win_start, void *d_workspace, size_t workspace_bytes,
                                             void *hip_stream);
+/* Synchronous forms: mem = SHF_HASH_MEM_DEVICE (every pointer on the device)
+ * or SHF_HASH_MEM_HOST (keys, offsets, out, perm and win_start in host memory:
+ * the records come back through the hashing pipeline while each key's window
+ * byte stays on the device, so they are never copied back in to be ordered --
+ * hash + shf_win_order(SHF_HASH_MEM_HOST) move 16 + 4 B per key more over PCIe).
+ * win_start may be NULL. The workspace is the library's, kept per thread and
+ * device. Variable-length keys with invalid offsets: SHF_HB_ERR_ARG (host memory:
+ * checked before anything is copied). */
+SHF_HB_API int shf_hash_batch_fixed_win(const void *keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                        shf_hash128 *out, uint32_t *perm, uint32_t *win_start, int mem);
+SHF_HB_API int shf_hash_batch_var_win(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
+                                      shf_hash128 *out, uint32_t *perm, uint32_t *win_start, int mem);
 /* The same with a forced hashing kernel (tests and benchmarks; SHF_HB_KERNEL_*). */
 SHF_HB_API int shf_hash_batch_fixed_win_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n,
                                                      uint32_t seed, shf_hash128 *d_out, uint32_t *d_perm,

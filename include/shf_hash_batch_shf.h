@@ -129,9 +129,9 @@ static inline uint64_t shf_get_batch_probed(SHF *shf, const char *bytes, const u
     return found;
 }
 
-/* shf_put_batch_var() in window order: one GPU batch hash, the GPU's window
- * order of those hashes (shf_win_order), then shf_put_key_val() per key in
- * that order. Keys of one window keep their batch order and windows share no
+/* shf_put_batch_var() in window order: one GPU call hashes the batch and
+ * orders it by window (shf_hash_batch_var_win: only the records and the order
+ * cross PCIe), then shf_put_key_val() per key in that order. Keys of one window keep their batch order and windows share no
  * state, so the store (files, uids) ends exactly as shf_put_batch_var() leaves
  * it. Returns n, the number of puts made before the first one that did not
  * return SHF_RET_KEY_PUT (in window order: which keys went in is then
@@ -149,8 +149,7 @@ static inline int64_t shf_put_batch_var_win_ordered(SHF *shf, const char *bytes,
         if (!perm_out) free(perm);
         return SHF_HB_ERR_NOMEM;
     }
-    int rc = shf_hash_batch_var(bytes, offsets, n, SHF_HASH_BATCH_SEED, h, SHF_HASH_MEM_HOST);
-    if (rc == SHF_HB_OK) rc = shf_win_order(h, n, perm, NULL, SHF_HASH_MEM_HOST);
+    int rc = shf_hash_batch_var_win(bytes, offsets, n, SHF_HASH_BATCH_SEED, h, perm, NULL, SHF_HASH_MEM_HOST);
     uint64_t j = 0;
     if (rc == SHF_HB_OK)
         for (; j < n; ++j) {

@@ -97,6 +97,8 @@ _SIGS = {
     "shf_win_order_workspace_bytes": [_U64],
     "shf_win_order_async": [_VP, _U64, _VP, _VP, _VP, ctypes.c_size_t, _VP],
     "shf_win_order": [_VP, _U64, _VP, _VP, _INT],
+    "shf_hash_batch_fixed_win": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _INT],
+    "shf_hash_batch_var_win": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _INT],
     "shf_hash_batch_fixed_win_async": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP],
     "shf_hash_batch_var_win_async": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP],
     "shf_hash_batch_fixed_win_kernel_async": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _INT,
@@ -551,6 +553,37 @@ def hash_var_win(data, offsets, seed=SEED, out=None, perm=None, win_start=None, 
     if stream is not None and own_ws:
         workspace.record_stream(stream)
     return out, perm, win_start
+
+
+def hash_fixed_win_host(keys, key_len=None, seed=SEED):
+    """Host keys in; host (hashes (n, 2) uint64, perm uint32[n], win_start uint32[257]) out
+    (shf_hash_batch_fixed_win, SHF_HASH_MEM_HOST: the window bytes stay on the device)."""
+    keys = _np_u8(keys)
+    if key_len is None:
+        key_len = keys.shape[-1] if keys.ndim == 2 else 16
+    flat = keys.reshape(-1)
+    n = flat.size // key_len if key_len else 0
+    out = np.empty((n, 2), dtype=np.uint64)
+    perm = np.empty(n, dtype=np.uint32)
+    ws = np.empty(257, dtype=np.uint32)
+    rc = load().shf_hash_batch_fixed_win(flat.ctypes.data, key_len, n, seed, out.ctypes.data, perm.ctypes.data,
+                                         ws.ctypes.data, MEM_HOST)
+    _check(rc, "shf_hash_batch_fixed_win")
+    return out, perm, ws
+
+
+def hash_var_win_host(data, offsets, seed=SEED):
+    """Variable-length host keys: (hashes, perm, win_start) (shf_hash_batch_var_win, SHF_HASH_MEM_HOST)."""
+    data = _np_u8(data).reshape(-1)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = off.size - 1
+    out = np.empty((n, 2), dtype=np.uint64)
+    perm = np.empty(n, dtype=np.uint32)
+    ws = np.empty(257, dtype=np.uint32)
+    rc = load().shf_hash_batch_var_win(data.ctypes.data, off.ctypes.data, n, seed, out.ctypes.data,
+                                       perm.ctypes.data, ws.ctypes.data, MEM_HOST)
+    _check(rc, "shf_hash_batch_var_win")
+    return out, perm, ws
 
 
 def win_order_host(hashes):

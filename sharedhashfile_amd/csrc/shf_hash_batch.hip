@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -134,6 +135,8 @@ struct DevCtx {
   uint32_t* h_status = nullptr;  // pinned, 1 word
   void* d_win_ws = nullptr;      // shf_win_order's workspace, kept across calls (grows only)
   size_t win_ws_cap = 0;
+  uint32_t* d_perm = nullptr;    // host-memory window orders: the order on the device (+ 257 starts)
+  size_t perm_cap = 0;
 };
 
 void release_ctx(DevCtx* c);
@@ -223,6 +226,7 @@ void release_ctx(DevCtx* c) {
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->d_win_ws) (void)hipFree(c->d_win_ws);
+  if (c->d_perm) (void)hipFree(c->d_perm);
   (void)hipGetLastError();
   (void)hipSetDevice(prev);
   delete c;
@@ -262,12 +266,28 @@ int ensure_win_ws(DevCtx* c, size_t bytes, void** out) {
     for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
     HB_TRY(hipStreamSynchronize(nullptr));
     if (c->d_win_ws) (void)hipFree(c->d_win_ws);
+  if (c->d_perm) (void)hipFree(c->d_perm);
     c->d_win_ws = nullptr;
     c->win_ws_cap = 0;
     HB_TRY(hipMalloc(&c->d_win_ws, bytes));
     c->win_ws_cap = bytes;
   }
   *out = c->d_win_ws;
+  return SHF_HB_OK;
+}
+
+// Device room for a host-memory window order: n indices then 257 window starts (grows only).
+int ensure_perm(DevCtx* c, uint64_t n, uint32_t** out) {
+  const size_t need = ((size_t)n + 257u) * sizeof(uint32_t);
+  if (need > c->perm_cap) {
+    for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
+    if (c->d_perm) (void)hipFree(c->d_perm);
+    c->d_perm = nullptr;
+    c->perm_cap = 0;
+    HB_TRY(hipMalloc((void**)&c->d_perm, need));
+    c->perm_cap = need;
+  }
+  *out = c->d_perm;
   return SHF_HB_OK;
 }
 
@@ -408,6 +428,7 @@ struct HostJob {
   bool stage_direct = false;         // else (pageable `hash`): the kernel stores into the slot's pinned staging
   shf_probe* probe = nullptr;
   const shf_row_index* index = nullptr;  // with probe
+  uint8_t* wins = nullptr;  // device: the batch's window bytes (kOutHashWin), key i's at wins[i]
 };
 
 // One chunk in flight per slot; `pending` remembers where its results go.
@@ -418,11 +439,39 @@ struct Pending {
   uint64_t count = 0;
 };
 
+// SHF_HB_TRACE=1 (read once): each host-pipeline call prints one line on
+// stderr with where its time went -- staging copies in, waits for the device,
+// copies out -- so a slow call can be told apart (tools/diag_pageable_staged.py).
+bool trace_on() {
+  static const bool on = [] {
+    const char* e = getenv("SHF_HB_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+struct PipeTrace {
+  double copy_in = 0, wait = 0, copy_out = 0, enqueue = 0;
+  uint64_t chunks = 0;
+};
+thread_local PipeTrace tls_trace;
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int drain_slot(DevCtx* c, int s, Pending& p) {
   if (!p.busy) return SHF_HB_OK;
+  const bool tr = trace_on();
+  const double t0 = tr ? now_ms() : 0;
   HB_TRY(hipEventSynchronize(c->done[s]));
+  const double t1 = tr ? now_ms() : 0;
   if (p.hash) par_memcpy(p.hash, c->h_out[s], p.count * sizeof(shf_hash128));
   if (p.probe) par_memcpy(p.probe, c->h_probe[s], p.count * sizeof(shf_probe));
+  if (tr) {
+    tls_trace.wait += t1 - t0;
+    tls_trace.copy_out += now_ms() - t1;
+  }
   p.busy = false;
   return SHF_HB_OK;
 }
@@ -447,7 +496,19 @@ void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k,
     void* staged = job.stage_direct ? host_range_device_ptr(c->h_out[s], sizeof(shf_hash128)) : nullptr;
     k->out = job.hash_dev ? job.hash_dev + i0 : staged ? staged : c->d_out[s];
     *mode = shfhb::kOutHash;
+    if (job.wins) {
+      k->wins = job.wins + i0;
+      *mode = shfhb::kOutHashWin;
+    }
   }
+}
+
+// The sink of a whole-batch launch straight into the caller's records (zero copy).
+int direct_sink(const HostJob& job, void* d_out, shfhb::Sink* k) {
+  *k = out_sink(d_out);
+  if (!job.wins) return shfhb::kOutHash;
+  k->wins = job.wins;
+  return shfhb::kOutHashWin;
 }
 
 // Results of chunk [i0, i0 + cnt) back to the caller (straight into page-locked
@@ -623,15 +684,19 @@ int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_l
     return 1;  // e.g. already page-locked by someone else: the staged pipeline instead
   const uint8_t* dk = static_cast<const uint8_t*>(lk.dev) + (kb + lo * key_len - kp0);
   shf_hash128* dh = reinterpret_cast<shf_hash128*>(static_cast<uint8_t*>(lo_.dev) + (ob + lo * 16 - op0));
-  HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, out_sink(dh), shfhb::kOutHash, c->st[0],
-                             shfhb::kKernelAuto));
+  shfhb::Sink mk;
+  int mmode = direct_sink(job, dh, &mk);
+  if (mk.wins) mk.wins += lo;
+  HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, mk, mmode, c->st[0], shfhb::kKernelAuto));
   // the ends meanwhile, through the staged pipeline (its slots queue behind the launch on st[0]),
   // copied through the staging as pageable memory: they may begin inside the pages just locked and
   // run past them, so they must not be taken for page-locked buffers
   int rc = SHF_HB_OK;
-  if (lo) rc = host_fixed_run(keys, key_len, lo, seed, hash_job(job.hash), false);
-  if (rc == SHF_HB_OK && hi < n)
-    rc = host_fixed_run(keys + hi * key_len, key_len, n - hi, seed, hash_job(job.hash + hi), false);
+  HostJob head = hash_job(job.hash), tail = hash_job(job.hash + hi);
+  head.wins = job.wins;
+  tail.wins = job.wins ? job.wins + hi : nullptr;
+  if (lo) rc = host_fixed_run(keys, key_len, lo, seed, head, false);
+  if (rc == SHF_HB_OK && hi < n) rc = host_fixed_run(keys + hi * key_len, key_len, n - hi, seed, tail, false);
   const hipError_t se = hipStreamSynchronize(c->st[0]);  // before the pages are unlocked
   if (rc) return rc;
   HB_TRY(se);
@@ -651,7 +716,9 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     void* dk = host_range_device_ptr(keys, (size_t)n * key_len);
     void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)) : nullptr;
     if (dh) {
-      HB_TRY(shfhb::launch_fixed(dk, key_len, n, seed, out_sink(dh), shfhb::kOutHash, c->st[0], shfhb::kKernelAuto));
+      shfhb::Sink dsk;
+      const int dmode = direct_sink(job, dh, &dsk);
+      HB_TRY(shfhb::launch_fixed(dk, key_len, n, seed, dsk, dmode, c->st[0], shfhb::kKernelAuto));
       HB_TRY(hipStreamSynchronize(c->st[0]));
       return SHF_HB_OK;
     }
@@ -676,13 +743,20 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     const uint64_t cnt = std::min(chunk, n - i0);
     const size_t nb = (size_t)cnt * key_len;
     const uint8_t* src = in_pinned ? keys + i0 * key_len : c->h_in[s];
+    const double t0 = trace_on() ? now_ms() : 0;
     if (nb && !in_pinned) par_memcpy(c->h_in[s], keys + i0 * key_len, nb);
+    const double t1 = trace_on() ? now_ms() : 0;
     if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], src, nb, hipMemcpyHostToDevice, c->st[s]));
     shfhb::Sink k;
     int mode = 0;
     job_sink(c, s, job, i0, &k, &mode);
     HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto));
     if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
+    if (trace_on()) {
+      tls_trace.copy_in += t1 - t0;
+      tls_trace.enqueue += now_ms() - t1;
+      ++tls_trace.chunks;
+    }
   }
   for (int s = 0; s < ns; ++s)
     if ((rc = drain_slot(c, s, pend[s]))) return rc;
@@ -778,7 +852,16 @@ int drain_on_error(int rc) {
 }
 
 int host_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
-  return drain_on_error(host_fixed_run(keys, key_len, n, seed, job));
+  if (!trace_on()) return drain_on_error(host_fixed_run(keys, key_len, n, seed, job));
+  tls_trace = PipeTrace();
+  const double t0 = now_ms();
+  const int rc = drain_on_error(host_fixed_run(keys, key_len, n, seed, job));
+  fprintf(stderr,
+          "shf_hash_batch trace: fixed n=%llu chunks=%llu total_ms=%.3f copy_in_ms=%.3f enqueue_ms=%.3f "
+          "wait_ms=%.3f copy_out_ms=%.3f rc=%d\n",
+          (unsigned long long)n, (unsigned long long)tls_trace.chunks, now_ms() - t0, tls_trace.copy_in,
+          tls_trace.enqueue, tls_trace.wait, tls_trace.copy_out, rc);
+  return rc;
 }
 
 int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job) {
@@ -1081,6 +1164,78 @@ int shf_hash_batch_var_win_async(const void* d_bytes, const uint64_t* d_offsets,
                                  size_t workspace_bytes, void* hip_stream) {
   return shf_hash_batch_var_win_kernel_async(d_bytes, d_offsets, n, seed, d_out, d_perm, d_win_start, d_workspace,
                                              workspace_bytes, SHF_HB_KERNEL_AUTO, hip_stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Synchronous hash + window order (shf_hash_batch_{fixed,var}_win). Device
+// memory: the async entry point on the context's stream, then a wait. Host
+// memory: the host pipelines hash into `out` and leave each key's window byte
+// in the device workspace (the records are never copied back in to be
+// ordered), the order is made on the device, and only perm / win_start come
+// back.
+int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n, uint32_t seed,
+                  shf_hash128* out, uint32_t* perm, uint32_t* win_start, int mem) {
+  if (mem != SHF_HASH_MEM_DEVICE && mem != SHF_HASH_MEM_HOST) return SHF_HB_ERR_ARG;
+  if (n == 0 && !win_start) return SHF_HB_OK;
+  if (n > 0xffffffffull || (!var && key_len > kMaxKeyLen)) return SHF_HB_ERR_ARG;
+  if (n && (!out || !perm || (var ? (!keys || !offsets) : (!keys && key_len)))) return SHF_HB_ERR_ARG;
+  DevCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  if (var && mem == SHF_HASH_MEM_HOST && (rc = check_var_lengths_host(offsets, n))) return rc;
+  void* ws = nullptr;
+  if ((rc = ensure_win_ws(c, (size_t)shfhb::win_order_workspace_bytes(n), &ws))) return rc;
+  const hipStream_t st = c->st[0];
+  if (mem == SHF_HASH_MEM_DEVICE) {
+    shfhb::Sink k = out_sink(out);
+    bool hist_done = false;
+    if (n) {
+      k.wins = shfhb::win_order_wins(ws, n);
+      if (var) {
+        k.status = c->d_status + 1;
+        HB_TRY(hipMemsetAsync(k.status, 0, sizeof(uint32_t), st));
+        HB_TRY(shfhb::launch_var(keys, offsets, 0, n, seed, k, shfhb::kOutHashWin, st));
+      } else {
+        k.win_counts = shfhb::win_order_counts(ws);
+        HB_TRY(shfhb::launch_fixed_win(keys, key_len, n, seed, k, st, shfhb::kKernelAuto, &hist_done));
+      }
+    }
+    HB_TRY(shfhb::launch_win_order_bytes(n, hist_done, perm, win_start, ws, st));
+    if (var && n) HB_TRY(hipMemcpyAsync(c->h_status, k.status, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HB_TRY(hipStreamSynchronize(st));
+    return var && n && *c->h_status ? SHF_HB_ERR_ARG : SHF_HB_OK;
+  }
+  uint32_t* d_perm = nullptr;
+  if ((rc = ensure_perm(c, n, &d_perm))) return rc;
+  if (n) {
+    HostJob job = hash_job(out);
+    job.wins = shfhb::win_order_wins(ws, n);
+    rc = var ? host_var((const uint8_t*)keys, offsets, n, seed, job)
+             : host_fixed((const uint8_t*)keys, key_len, n, seed, job);
+    if (rc) return rc;
+  }
+  HB_TRY(shfhb::launch_win_order_bytes(n, false, d_perm, d_perm + n, ws, st));
+  if (n) HB_TRY(hipMemcpyAsync(perm, d_perm, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (win_start) HB_TRY(hipMemcpyAsync(win_start, d_perm + n, 257u * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HB_TRY(hipStreamSynchronize(st));
+  return SHF_HB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shf_hash_batch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
+                             uint32_t* perm, uint32_t* win_start, int mem) {
+  return hash_win_sync(false, keys, nullptr, key_len, n, seed, out, perm, win_start, mem);
+}
+
+int shf_hash_batch_var_win(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out,
+                           uint32_t* perm, uint32_t* win_start, int mem) {
+  return hash_win_sync(true, bytes, offsets, 0, n, seed, out, perm, win_start, mem);
 }
 
 int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,

@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "../../include/shf_hash_batch.h"
 #include "kernels.h"
 
@@ -294,9 +296,12 @@ __device__ __forceinline__ uint64_t match_byte(uint32_t w) {
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)w, b, 1);  // 0 or ~0: this lane's bit b
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(m != 0u);
-    lo = __builtin_amdgcn_bitop3_b32(lo, m, (uint32_t)bal, 0xF6);          // lo | (m ^ bal)
+    // m = 0 or ~0 (this lane's bit b), bal = the lanes whose bit b is set: two VALU ops
+    // (written out: the compiler's own sequence for the same ballot takes three)
+    uint32_t m;
+    uint64_t bal;
+    asm volatile("v_bfe_i32 %0, %2, %3, 1\n\tv_cmp_ne_u32_e64 %1, 0, %0" : "=&v"(m), "=s"(bal) : "v"(w), "n"(b));
+    lo = __builtin_amdgcn_bitop3_b32(lo, m, (uint32_t)bal, 0xF6);  // lo | (m ^ bal)
     hi = __builtin_amdgcn_bitop3_b32(hi, m, (uint32_t)(bal >> 32), 0xF6);
   }
   return ~(((uint64_t)hi << 32) | lo);
@@ -322,10 +327,14 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t*
   const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
   const uint64_t k0 = (uint64_t)c * kWoChunk;
   const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
   const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
-  const uint32_t tot = row[gridDim.x];
-  const uint32_t pre = row[c];
+  u32x4 cwv = {t * 0x01010101u, 0u, 0u, 0u};
+  uint32_t tot = 4096u, pre = c * 16u;
+  if (!(dbg & 32)) {
+    cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
+    tot = row[gridDim.x];
+    pre = row[c];
+  }
   cw[4u * t + 0] = cwv.x;
   cw[4u * t + 1] = cwv.y;
   cw[4u * t + 2] = cwv.z;
@@ -339,12 +348,19 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t*
 #pragma unroll
   for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
   // (1) ranks within the wave
-  if (!(dbg & 1))
+  if (dbg & 1) {
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) rk[st] = 64u * st + lane;
+  } else
 #pragma unroll
   for (uint32_t st = 0; st < kWoSub / 64; ++st) {
     const bool valid = s0 + 64u * st + lane < s1;
-    const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
+    const uint64_t peers = ((dbg & 128) ? (1ull << lane) : match_byte(ws[st])) & __builtin_amdgcn_ballot_w64(valid);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+    if (dbg & 64) {
+      rk[st] = rank + (uint32_t)__popcll(peers);
+      continue;
+    }
     const uint32_t base = cnt[wave][ws[st]];
     rk[st] = base + rank;
     if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
@@ -359,6 +375,7 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t*
     hc += hv[v];
   }
   uint32_t it = tot, ih = hc;
+  if (!(dbg & 16))
 #pragma unroll
   for (uint32_t d = 1; d < 64; d <<= 1) {
     const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
@@ -386,7 +403,7 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t*
     uint32_t run = lbase;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      cnt[v][t] = run;
+      cnt[v][t] = (dbg & 1) ? 0u : run;
       run += hv[v];
     }
   }
@@ -407,7 +424,250 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t*
   for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
     const uint32_t j = t + kWoThreads * q;
     const uint32_t g = (dbg & 4) ? (uint32_t)k0 + j : min(gdelta[(e[q] >> 16) & 255u] + j, (uint32_t)n - 1u);
+    if (j < kn && (!(dbg & 8) || e[q] == 0xffffffffu)) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
+  }
+}
+
+// k_wo_scatter with each step's ranks taken from LDS atomics that return the
+// old count (ds_add_rtn_u32: one instruction per step, no ballots): lanes of a
+// step that share a window get consecutive counts, and the stable order needs
+// them in lane order. The order is then checked where it is written out (each
+// window's run of the sorted chunk must hold increasing key offsets: with the
+// counts exact, that is exactly the stable order); a chunk that fails the
+// check is ordered again with ballots (k_wo_scatter_ballot's ranks), so the
+// result never depends on the order the LDS unit serves same-address lanes in.
+__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_fast(const uint8_t* __restrict__ wins, uint64_t n,
+                                                               const uint32_t* __restrict__ counts,
+                                                               uint32_t* __restrict__ perm,
+                                                               uint32_t* __restrict__ win_start, uint32_t dbg) {
+  __shared__ uint32_t cnt[4][kWoBins];
+  __shared__ uint32_t cw[kWoChunk / 4];
+  __shared__ uint32_t sorted[kWoChunk];
+  __shared__ uint32_t gdelta[kWoBins];
+  __shared__ uint32_t tsum[2][4];
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
+  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
+  const uint64_t k0 = (uint64_t)c * kWoChunk;
+  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
+  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
+  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
+  const uint32_t tot = row[gridDim.x];
+  const uint32_t pre = row[c];
+  cw[4u * t + 0] = cwv.x;
+  cw[4u * t + 1] = cwv.y;
+  cw[4u * t + 2] = cwv.z;
+  cw[4u * t + 3] = cwv.w;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
+  __syncthreads();
+  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
+  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
+  uint32_t ws[kWoSub / 64], rk[kWoSub / 64];
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
+  // (1) ranks within the wave: the window's count so far, one atomic per step
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st)
+    rk[st] = s0 + 64u * st + lane < s1 ? atomicAdd(&cnt[wave][ws[st]], 1u) : 0u;
+  for (int pass = 0;; ++pass) {
+    __syncthreads();
+    // (2) window t: its keys in the chunk and in waves 0..v-1; exclusive scans over
+    // the windows of the totals (its base in perm) and of the chunk counts (its local start)
+    uint32_t hv[4], hc = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      hv[v] = cnt[v][t];
+      hc += hv[v];
+    }
+    uint32_t it = tot, ih = hc;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
+      if (lane >= d) {
+        it += ut;
+        ih += uh;
+      }
+    }
+    if (lane == 63) {
+      tsum[0][wave] = it;
+      tsum[1][wave] = ih;
+    }
+    __syncthreads();
+    uint32_t bbase = it - tot, lbase = ih - hc;
+    for (uint32_t v = 0; v < wave; ++v) {
+      bbase += tsum[0][v];
+      lbase += tsum[1][v];
+    }
+    if (c == 0 && win_start && pass == 0) {
+      win_start[t] = bbase;
+      if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
+    }
+    gdelta[t] = bbase + pre - lbase;
+    {
+      uint32_t run = lbase;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        cnt[v][t] = run;
+        run += hv[v];
+      }
+    }
+    __syncthreads();
+    // (3) the chunk's window order, in LDS
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+      const uint32_t i = s0 + 64u * st + lane;
+      if (i < s1) sorted[cnt[wave][ws[st]] + rk[st]] = i | (ws[st] << 16);
+    }
+    __syncthreads();
+    // the check: within each window's run, key offsets increase
+    bool bad = false;
+#pragma unroll
+    for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
+      const uint32_t j = t + kWoThreads * q;
+      if (j != 0 && j < kn) {
+        const uint32_t a = sorted[j - 1], b = sorted[j];
+        bad |= (a >> 16) == (b >> 16) && (a & 0xffffu) > (b & 0xffffu);
+      }
+    }
+    if (!__syncthreads_or((int)bad) || pass == 1 || (dbg & 1)) break;
+    // fallback: ranks from ballots (as k_wo_scatter_ballot), counts rebuilt from zero
+#pragma unroll
+    for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+      const bool valid = s0 + 64u * st + lane < s1;
+      const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+      const uint32_t base = cnt[wave][ws[st]];
+      rk[st] = base + rank;
+      if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
+    }
+  }
+  // (4) out in that order: local position j holds key offset i of window w
+  uint32_t e[kWoChunk / kWoThreads];
+#pragma unroll
+  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) e[q] = sorted[min(t + kWoThreads * q, kn - 1u)];
+#pragma unroll
+  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
+    const uint32_t j = t + kWoThreads * q;
+    const uint32_t g = gdelta[e[q] >> 16] + j;
     if (j < kn) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
+  }
+}
+
+// Persistent variant of k_wo_scatter_ballot: gridDim.x workgroups (a multiple
+// of 8), workgroup g on XCD g % 8 walks that XCD's contiguous range of chunks
+// with a stride of the XCD's workgroups, and loads the next chunk's window bytes
+// and prefixes before ordering the current one (the loads of a chunk are a
+// latency the order of the previous one hides). A lane reads its own 16
+// window bytes (one per step) straight from the workspace: no LDS copy.
+__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_pf(const uint8_t* __restrict__ wins, uint64_t n,
+                                                             uint32_t chunks, const uint32_t* __restrict__ counts,
+                                                             uint32_t* __restrict__ perm,
+                                                             uint32_t* __restrict__ win_start, uint32_t dbg) {
+  __shared__ uint32_t cnt[4][kWoBins];
+  __shared__ uint32_t sorted[kWoChunk];
+  __shared__ uint32_t gdelta[kWoBins];
+  __shared__ uint32_t tsum[2][4];
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
+  const uint32_t G = gridDim.x, x = blockIdx.x % 8u, gi = blockIdx.x / 8u, P = G / 8u;
+  const uint32_t q = chunks / 8u, r8 = chunks % 8u;
+  const uint32_t xc0 = x * q + min(x, r8), xc1 = xc0 + q + (x < r8 ? 1u : 0u);  // this XCD's chunks
+  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(chunks);
+  const uint32_t tot = row[chunks];
+  uint32_t c = xc0 + gi;
+  uint32_t nws[kWoSub / 64], npre = 0;
+  auto fetch = [&](uint32_t cc) {
+    const uint64_t kb = (uint64_t)cc * kWoChunk + kWoSub * wave + lane;
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) nws[st] = wins[kb + 64u * st];
+    npre = row[cc];
+  };
+  if (c < xc1) fetch(c);
+  for (; c < xc1; c += P) {
+    uint32_t ws[kWoSub / 64];
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = nws[st];
+    const uint32_t pre = npre;
+    if (c + P < xc1) fetch(c + P);
+    const uint64_t k0 = (uint64_t)c * kWoChunk;
+    const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
+    __syncthreads();
+    const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
+    uint32_t rk[kWoSub / 64];
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+      if (dbg & 1) {
+        rk[st] = 64u * st + lane;
+        continue;
+      }
+      const bool valid = s0 + 64u * st + lane < s1;
+      const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+      const uint32_t base = cnt[wave][ws[st]];
+      rk[st] = base + rank;
+      if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    uint32_t hv[4], hc = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      hv[v] = cnt[v][t];
+      hc += hv[v];
+    }
+    uint32_t it = tot, ih = hc;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
+      if (lane >= d) {
+        it += ut;
+        ih += uh;
+      }
+    }
+    if (lane == 63) {
+      tsum[0][wave] = it;
+      tsum[1][wave] = ih;
+    }
+    __syncthreads();
+    uint32_t bbase = it - tot, lbase = ih - hc;
+    for (uint32_t v = 0; v < wave; ++v) {
+      bbase += tsum[0][v];
+      lbase += tsum[1][v];
+    }
+    if (c == 0 && win_start) {
+      win_start[t] = bbase;
+      if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
+    }
+    gdelta[t] = bbase + pre - lbase;
+    {
+      uint32_t run = lbase;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        cnt[v][t] = (dbg & 1) ? 0u : run;
+        run += hv[v];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+      const uint32_t i = s0 + 64u * st + lane;
+      if (i < s1) sorted[(dbg & 1) ? i : cnt[wave][ws[st]] + rk[st]] = i | (ws[st] << 16);
+    }
+    __syncthreads();
+    uint32_t e[kWoChunk / kWoThreads];
+#pragma unroll
+    for (uint32_t qq = 0; qq < kWoChunk / kWoThreads; ++qq) e[qq] = sorted[min(t + kWoThreads * qq, kn - 1u)];
+#pragma unroll
+    for (uint32_t qq = 0; qq < kWoChunk / kWoThreads; ++qq) {
+      const uint32_t j = t + kWoThreads * qq;
+      const uint32_t g = (dbg & 4) ? (uint32_t)k0 + j : min(gdelta[(e[qq] >> 16) & 255u] + j, (uint32_t)n - 1u);
+      if (j < kn) perm[g] = (uint32_t)(k0 + (e[qq] & 0xffffu));
+    }
+    // the next chunk's first LDS writes (cnt) follow every wave's reads of this one's
+    __syncthreads();
   }
 }
 
@@ -445,6 +705,15 @@ hipError_t launch_win_order_bytes(uint64_t n, bool hist_done, uint32_t* perm, ui
   if (e && e[0] == '2')
     hipLaunchKernelGGL(k_wo_scatter_ballot, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start,
                        (uint32_t)atoi(e + 1));
+  else if (e && e[0] == '4')
+    hipLaunchKernelGGL(k_wo_scatter_fast, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start,
+                       (uint32_t)atoi(e + 1));
+  else if (e && e[0] == '3') {  // 3<wgs per CU><dbg>
+    const uint32_t per_cu = (uint32_t)(e[1] - '0');
+    const uint32_t g = std::min<uint32_t>((chunks + 7u) / 8u * 8u, 256u * per_cu);
+    hipLaunchKernelGGL(k_wo_scatter_pf, dim3(g), dim3(kWoThreads), 0, st, wins, n, chunks, counts, perm, win_start,
+                       (uint32_t)atoi(e + 2));
+  }
   else
     hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
   return hipGetLastError();

@@ -352,3 +352,66 @@ def test_fused_rejects_bad_arguments(hb, dev):
         assert f(vp(keys), 16, n, 12345, vp(out), vp(p), None, vp(ws), need, None) == hb.OK
     torch.cuda.synchronize(dev)
     assert (s == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 4097, 70_000, 2_500_003])
+def test_fused_sync_host_fixed(hb, dev, oracle, n):
+    """shf_hash_batch_fixed_win(SHF_HASH_MEM_HOST) over pageable, page-locked and
+    odd-sized batches (the zero-copy, pageable zero-copy and staged pipelines all
+    write the window bytes into the device workspace)."""
+    import torch
+
+    rng = np.random.default_rng(n + 5)
+    keys = rng.integers(0, 256, size=n * 16, dtype=np.uint8)
+    want = oracle.hash_fixed(keys, 16)
+    ref_perm, ref_start = Oracle.win_order(want)
+    for src in (keys, torch.from_numpy(keys.copy()).pin_memory().numpy()):
+        h, perm, start = hb.hash_fixed_win_host(src.reshape(n, 16))
+        np.testing.assert_array_equal(h, want)
+        np.testing.assert_array_equal(perm, ref_perm)
+        np.testing.assert_array_equal(start, ref_start)
+    h, perm, start = hb.hash_fixed_win_host(np.frombuffer(keys.tobytes()[: 37 * (n // 37) * 1], dtype=np.uint8)
+                                            .reshape(-1, 37) if n >= 37 else keys[:37].reshape(1, 37))
+    flat = keys[: h.shape[0] * 37]
+    np.testing.assert_array_equal(h, oracle.hash_fixed(flat, 37))
+    np.testing.assert_array_equal(perm, Oracle.win_order(h)[0])
+
+
+@pytest.mark.gpu
+def test_fused_sync_host_var_and_device(hb, dev, oracle):
+    import ctypes
+
+    import torch
+
+    data, off = _unique_keys(300_000, 23, 0, 600)
+    want = oracle.hash_var(data, off)
+    ref_perm, ref_start = Oracle.win_order(want)
+    h, perm, start = hb.hash_var_win_host(data, off)
+    np.testing.assert_array_equal(h, want)
+    np.testing.assert_array_equal(perm, ref_perm)
+    np.testing.assert_array_equal(start, ref_start)
+    # device memory, synchronous
+    n = off.size - 1
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(off.view(np.int64)).to(dev)
+    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    p = torch.empty(n, dtype=torch.int32, device=dev)
+    s = torch.empty(257, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    with torch.cuda.device(dev):
+        assert hb.load().shf_hash_batch_var_win(vp(d), vp(o), n, 12345, vp(out), vp(p), vp(s), hb.MEM_DEVICE) == 0
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), want)
+    np.testing.assert_array_equal(p.cpu().numpy().view(np.uint32), ref_perm)
+    np.testing.assert_array_equal(s.cpu().numpy().view(np.uint32), ref_start)
+    # a decreasing offset: refused before anything moves (host), flagged by the kernels (device)
+    bad = off.copy()
+    bad[10] = bad[12]
+    with pytest.raises(hb.ShfHashBatchError):
+        hb.hash_var_win_host(data, bad)
+    ob = torch.from_numpy(bad.view(np.int64)).to(dev)
+    with torch.cuda.device(dev):
+        assert hb.load().shf_hash_batch_var_win(vp(d), vp(ob), n, 12345, vp(out), vp(p), None, hb.MEM_DEVICE) \
+            == hb.ERR_ARG
+        assert hb.load().shf_hash_batch_fixed_win(vp(d), 16, 100, 12345, vp(out), vp(p), None, 9) == hb.ERR_ARG

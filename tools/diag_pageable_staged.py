@@ -38,6 +38,7 @@ def main():
     p.add_argument("--repeats", type=int, default=20)
     p.add_argument("--fresh-out", action="store_true", help="a new (never touched) output array every repeat")
     p.add_argument("--env", action="append", default=[], help="NAME=VALUE set before the calls")
+    p.add_argument("--trace-file", default=None, help="where this run's stderr goes (with SHF_HB_TRACE=1)")
     a = p.parse_args()
     os.environ["SHF_HB_PAGEABLE_ZERO_COPY"] = "0"
     for kv in a.env:
@@ -66,6 +67,12 @@ def main():
                      "cg_throttled": c1.get("nr_throttled", 0) - c0.get("nr_throttled", 0),
                      "cg_throttled_ms": round((c1.get("throttled_usec", 0) - c0.get("throttled_usec", 0)) / 1e3, 2)})
     v = np.array([x["gkeys_s"] for x in rows])
+    # SHF_HB_TRACE=1: the library's own per-call split (stderr lines, in call order)
+    if os.environ.get("SHF_HB_TRACE") == "1" and a.trace_file and os.path.exists(a.trace_file):
+        tr = [l for l in open(a.trace_file) if l.startswith("shf_hash_batch trace:")][-a.repeats:]
+        for row, line in zip(rows, tr):
+            row.update({kv.split("=")[0]: float(kv.split("=")[1]) for kv in line.split()[2:]
+                        if kv.split("=")[0].endswith("_ms")})
     summary = {"n": a.n, "fresh_out": a.fresh_out, "env": a.env, "median": float(np.median(v)), "min": float(v.min()),
                "max": float(v.max()), "spread_max_over_min": round(float(v.max() / v.min()), 3),
                "cgroup_cpu_max": open("/sys/fs/cgroup/cpu.max").read().strip() if os.path.exists(
