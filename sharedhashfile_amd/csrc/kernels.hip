@@ -1290,7 +1290,9 @@ hipError_t launch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint
   *hist_done = false;
   if (n == 0) return hipSuccess;
   const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
-  if (key_len == 16 && al16 && sink.win_counts && (kernel == kKernelAuto || kernel == kKernelFixed16)) {
+  const char* e0 = getenv("SHF_HB_F16WIN_BLOCK");  // EXPERIMENT: 0 = no fused histogram
+  if (key_len == 16 && al16 && sink.win_counts && (kernel == kKernelAuto || kernel == kKernelFixed16) &&
+      !(e0 && e0[0] == '0')) {
     const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
     if (chunks > 0x7fffffffull) return hipErrorInvalidValue;
     const char* e = getenv("SHF_HB_F16WIN_BLOCK");  // EXPERIMENT (removed once a shape is chosen)

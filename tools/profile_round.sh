@@ -11,7 +11,8 @@ export TMPDIR=/tmp
 common="--steps 20 --warmup 3 --repeats 1 --warmup-min-s 0.5 --no-cpu --no-verify --no-host-inclusive --traffic off"
 i=0
 for only in "fixed16" "ceil_copy,ceil_copy_hot,fixed16_hot" "shard1b,ceil_copy_1b" "fixed256,ceil_read16,ceil_read16nt,ceil_read16w1" \
-            "var" "probe16,ceil_gather128" "tabpart,ceil_copynt,ceil_stream16u" "winorder" "ceil_valu_add,ceil_valu_mul"; do
+            "var" "probe16,ceil_gather128" "probe16_hbm,ceil_probe_rows_hbm" "tabpart,ceil_copynt,ceil_stream16u" "winorder" \
+            "hashwin16" "ceil_valu_add,ceil_valu_mul"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt$i" -o kt -- \
     python3 bench.py $common --only "$only" > "$out/kt$i.json" 2> "$out/kt$i.err" || { echo "kt pass $i ($only) failed"; exit 1; }
