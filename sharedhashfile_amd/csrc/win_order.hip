@@ -675,6 +675,110 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_v(const uint8_t* __re
   }
 }
 
+// k_wo_scatter_ballot in one ordering pass: the waves' histograms first (LDS
+// adds, no return), so every wave's count per window starts at that window's
+// first local position for the wave; each step then places its keys directly
+// (base + rank among the step's peers) and the lowest peer advances the count.
+// Fewer LDS accesses at random addresses per key (about 4 instead of 5) and no
+// ranks held across barriers.
+__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_one(const uint8_t* __restrict__ wins, uint64_t n,
+                                                              const uint32_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ perm,
+                                                              uint32_t* __restrict__ win_start) {
+  __shared__ uint32_t cnt[4][kWoBins];
+  __shared__ uint32_t cw[kWoChunk / 4];
+  __shared__ uint32_t sorted[kWoChunk];
+  __shared__ uint32_t gdelta[kWoBins];
+  __shared__ uint32_t tsum[2][4];
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
+  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
+  const uint64_t k0 = (uint64_t)c * kWoChunk;
+  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
+  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
+  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
+  const uint32_t tot = row[gridDim.x];
+  const uint32_t pre = row[c];
+  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
+  cw[4u * t + 0] = cwv.x;
+  cw[4u * t + 1] = cwv.y;
+  cw[4u * t + 2] = cwv.z;
+  cw[4u * t + 3] = cwv.w;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
+  __syncthreads();
+  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
+  // the wave's histogram of its 1024 window bytes
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+    const uint32_t i = s0 + 64u * st + lane;
+    if (i < s1) atomicAdd(&cnt[wave][cwb[i]], 1u);
+  }
+  __syncthreads();
+  uint32_t hv[4], hc = 0;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    hv[v] = cnt[v][t];
+    hc += hv[v];
+  }
+  uint32_t it = tot, ih = hc;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
+    if (lane >= d) {
+      it += ut;
+      ih += uh;
+    }
+  }
+  if (lane == 63) {
+    tsum[0][wave] = it;
+    tsum[1][wave] = ih;
+  }
+  __syncthreads();
+  uint32_t bbase = it - tot, lbase = ih - hc;
+  for (uint32_t v = 0; v < wave; ++v) {
+    bbase += tsum[0][v];
+    lbase += tsum[1][v];
+  }
+  if (c == 0 && win_start) {
+    win_start[t] = bbase;
+    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
+  }
+  gdelta[t] = bbase + pre - lbase;
+  {
+    uint32_t run = lbase;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      cnt[v][t] = run;
+      run += hv[v];
+    }
+  }
+  __syncthreads();
+  // each step's keys straight to their local positions
+#pragma unroll
+  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
+    const uint32_t i = s0 + 64u * st + lane;
+    const uint32_t w = cwb[i];
+    const bool valid = i < s1;
+    const uint64_t peers = match_byte(w) & __builtin_amdgcn_ballot_w64(valid);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+    const uint32_t base = cnt[wave][w];
+    if (valid) sorted[base + rank] = i | (w << 16);
+    if (valid && rank == 0) cnt[wave][w] = base + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t q0 = 0; q0 < kWoChunk / kWoThreads; q0 += 8) {
+    uint32_t e[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) e[q] = sorted[min(t + kWoThreads * (q0 + q), kn - 1u)];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+      const uint32_t j = t + kWoThreads * (q0 + q);
+      if (j < kn) perm[gdelta[e[q] >> 16] + j] = (uint32_t)(k0 + (e[q] & 0xffffu));
+    }
+  }
+}
+
 // Persistent variant of k_wo_scatter_ballot: gridDim.x workgroups (a multiple
 // of 8), workgroup g on XCD g % 8 walks that XCD's contiguous range of chunks
 // with a stride of the XCD's workgroups, and loads the next chunk's window bytes
@@ -828,6 +932,8 @@ hipError_t launch_win_order_bytes(uint64_t n, bool hist_done, uint32_t* perm, ui
     hipLaunchKernelGGL(k_wo_scatter_v<1>, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
   else if (e && e[0] == '5' && e[1] == '2')
     hipLaunchKernelGGL(k_wo_scatter_v<2>, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
+  else if (e && e[0] == '6')
+    hipLaunchKernelGGL(k_wo_scatter_one, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
   else if (e && e[0] == '4')
     hipLaunchKernelGGL(k_wo_scatter_fast, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start,
                        (uint32_t)atoi(e + 1));

@@ -138,6 +138,23 @@ def test_argument_validation_needs_no_device(hb):
     assert lib.shf_row_index_set_tabs(None, keys.ctypes.data) == hbmod.ERR_ARG
     assert lib.shf_row_index_set_rows(None, 0, 1, keys.ctypes.data) == hbmod.ERR_ARG
     assert lib.shf_row_index_device_ptrs(None, None, None, None) == hbmod.ERR_ARG
+    # hash + window order: argument checks come before any device work
+    perm = np.zeros(4, dtype=np.uint32)
+    ws = np.zeros(1 << 20, dtype=np.uint8)
+    assert lib.shf_hash_batch_fixed_win_async(None, 16, 0, 12345, None, None, None, None, 0, None) == hbmod.OK
+    assert lib.shf_hash_batch_fixed_win_async(keys.ctypes.data, 16, 4, 12345, None, perm.ctypes.data, None,
+                                              ws.ctypes.data, ws.size, None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_fixed_win_async(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, perm.ctypes.data,
+                                              None, ws.ctypes.data, 16, None) == hbmod.ERR_ARG  # workspace too small
+    assert lib.shf_hash_batch_fixed_win_kernel_async(keys.ctypes.data, 17, 3, 12345, out.ctypes.data,
+                                                     perm.ctypes.data, None, ws.ctypes.data, ws.size,
+                                                     hbmod.KERNEL_FIXED16, None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_var_win_async(keys.ctypes.data, None, 2, 12345, out.ctypes.data, perm.ctypes.data,
+                                            None, ws.ctypes.data, ws.size, None) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_fixed_win(keys.ctypes.data, 16, 4, 12345, out.ctypes.data, perm.ctypes.data, None,
+                                        7) == hbmod.ERR_ARG
+    assert lib.shf_hash_batch_var_win(keys.ctypes.data, None, 2, 12345, out.ctypes.data, perm.ctypes.data, None,
+                                      hbmod.MEM_HOST) == hbmod.ERR_ARG
 
 
 @pytest.mark.skipif(_has_gpu(), reason="checks the no-device behaviour")
