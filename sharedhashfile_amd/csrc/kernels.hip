@@ -261,6 +261,10 @@ __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__
 // each hash record it writes the key's window byte and the chunk's 256-bin
 // histogram (LDS atomics, into the bin-major counts): the order passes then
 // never read the 16-B records back (win_order.hip).
+// 1024 threads (4 keys per lane): 256 threads (16 keys per lane) 63 us per 10M
+// keys, 512 60, 1024 59 (k_fixed16 alone 51; profiles/r4/win_order/README.md).
+constexpr uint32_t kF16WinBlock = 1024;
+
 template <uint32_t BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_fixed16_win(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
                                                        Sink sink) {
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(BLOCK) void k_fixed16_win(const u32x4* __restrict__
   __shared__ uint32_t hist[kWoBins];
   __shared__ __attribute__((aligned(16))) uint8_t cwb[kWoChunk];
   const uint32_t t = threadIdx.x;
-  const uint32_t c = sink.n_slots ? blockIdx.x : xcd_major(blockIdx.x, gridDim.x);  // EXPERIMENT: n_slots = plain map
+  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
   const uint64_t k0 = (uint64_t)c * kWoChunk;
   const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
   if (t < kWoBins) hist[t] = 0;
@@ -1290,20 +1294,11 @@ hipError_t launch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint
   *hist_done = false;
   if (n == 0) return hipSuccess;
   const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
-  const char* e0 = getenv("SHF_HB_F16WIN_BLOCK");  // EXPERIMENT: 0 = no fused histogram
-  if (key_len == 16 && al16 && sink.win_counts && (kernel == kKernelAuto || kernel == kKernelFixed16) &&
-      !(e0 && e0[0] == '0')) {
+  if (key_len == 16 && al16 && sink.win_counts && (kernel == kKernelAuto || kernel == kKernelFixed16)) {
     const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
     if (chunks > 0x7fffffffull) return hipErrorInvalidValue;
-    const char* e = getenv("SHF_HB_F16WIN_BLOCK");  // EXPERIMENT (removed once a shape is chosen)
-    const int blk = e ? atoi(e) : 256;
-    const char* pm = getenv("SHF_HB_F16WIN_PLAIN");
-    Sink sk = sink;
-    sk.n_slots = pm && pm[0] == '1';
-    const u32x4* k4 = reinterpret_cast<const u32x4*>(keys);
-    if (blk == 1024) hipLaunchKernelGGL(k_fixed16_win<1024>, dim3((unsigned)chunks), dim3(1024), 0, st, k4, n, seed, sk);
-    else if (blk == 512) hipLaunchKernelGGL(k_fixed16_win<512>, dim3((unsigned)chunks), dim3(512), 0, st, k4, n, seed, sk);
-    else hipLaunchKernelGGL(k_fixed16_win<256>, dim3((unsigned)chunks), dim3(256), 0, st, k4, n, seed, sk);
+    hipLaunchKernelGGL(k_fixed16_win<kF16WinBlock>, dim3((unsigned)chunks), dim3(kF16WinBlock), 0, st,
+                       reinterpret_cast<const u32x4*>(keys), n, seed, sink);
     *hist_done = true;
     return hipGetLastError();
   }

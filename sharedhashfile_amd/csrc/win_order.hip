@@ -11,23 +11,21 @@
 // consecutive operations then find the window's lock, map and tabs in cache:
 // the reference's get loop runs ~1.5x faster in window order.
 //
-// Four launches, HBM-bound (16-B hash records in, 4-B indices out; the
-// records are read once: 16 + 1 + 1 + 4 B per key against 20 B at least), one
-// workgroup of four waves per chunk of kWoChunk keys:
-//   k_wo_hist     the chunk's 256-bin histogram (LDS atomics) as one row of
-//                 counts[chunk][bin], and each key's window as one byte;
-//   k_wo_scan_*   the chunks' counts scanned per bin in two levels (blocks of
-//                 64 rows, then the blocks' sums), rows read whole;
-//   k_wo_scatter  the chunk's window bytes staged in LDS; each wave orders its
-//                 quarter, 64 keys per step (see the kernel).
-// Chunks are numbered XCD by XCD (workgroup g runs on XCD g % 8), so the runs
-// of positions that consecutive chunks write into one window's range are
-// written through the same L2 and leave HBM as whole lines.
+// Three launches, one workgroup of four waves per chunk of kWoChunk keys:
+//   k_wo_hist        (shf_win_order*) the chunk's 256-bin histogram (LDS
+//                    atomics) from its 16-B hash records, and each key's window
+//                    as one byte; or, when a hashing kernel has written the
+//                    window bytes beside its records (shf_hash_batch_*_win*,
+//                    kOutHashWin), k_wo_hist_bytes from those bytes (1 B per
+//                    key) -- or nothing, when the 16-B hashing kernel counted
+//                    the chunks itself (k_fixed16_win);
+//   k_wo_scan_rows   the bin-major counts scanned per window, one row each;
+//   k_wo_scatter     the chunk ordered in LDS, then written out in order.
+// Chunks are dealt to the XCDs in contiguous ranges (workgroup g runs on XCD
+// g % 8), so the runs of positions that consecutive chunks write into one
+// window's range, and the 128-B lines of the counts rows, fill through one L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
-
-#include <algorithm>
 
 #include "../../include/shf_hash_batch.h"
 #include "kernels.h"
@@ -159,136 +157,6 @@ __global__ __launch_bounds__(256) void k_wo_scan_rows(uint32_t* __restrict__ cou
   if (t == 0) row[chunks] = carry;
 }
 
-// One chunk per workgroup, in two phases. (1) The chunk's stable order in LDS:
-// wave v takes keys [1024 v, 1024 v + 1024) in key order, 64 per step; the
-// lanes of a step holding the same window find each other through a 64-bit LDS
-// mask per window (each sets its bit with an atomic OR -- an OR commutes, so
-// the order the LDS unit takes the lanes in does not matter -- then reads the
-// mask back), the lowest takes the window's next local positions for all of
-// them and clears the mask, and each lane puts its key at local start + its
-// rank among them. A window's first local position for wave v = the chunk's
-// keys of lower windows + the window's keys in waves 0..v-1 (histograms of the
-// chunk's window bytes). (2) The chunk's keys leave in that order, thread t
-// the positions t, t + 256, ...: a window's keys are consecutive both in LDS
-// and in perm (at the window's base, from the totals, + the chunk's prefix,
-// k_wo_scan_*), so each store instruction writes a few runs of whole lines
-// instead of one scattered index per lane (eight ballots per step instead of
-// the masks, with per-lane scattered stores: 47 us per 10M keys).
-// A wave's LDS accesses execute in order, and the compiler keeps the order of
-// these aliasing ones: no fence between steps.
-__global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __restrict__ wins, uint64_t n,
-                                                          const uint32_t* __restrict__ counts,
-                                                          uint32_t* __restrict__ perm,
-                                                          uint32_t* __restrict__ win_start) {
-  __shared__ uint32_t next[4][kWoBins];         // per wave: the window's next local position
-  __shared__ uint32_t cw[kWoChunk / 4];         // the chunk's window bytes
-  __shared__ uint32_t sorted[kWoChunk];         // the chunk's keys in window order: offset | window << 16
-  __shared__ uint32_t gdelta[kWoBins];          // window t's perm position minus its local one
-  __shared__ uint32_t tsum[2][4];
-  __shared__ uint64_t peer_mask[4][kWoBins];    // per wave: the lanes of this step holding each window
-  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
-  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
-  const uint64_t k0 = (uint64_t)c * kWoChunk;
-  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  // every global load first: the chunk's 4 KiB of window bytes (16 B per thread;
-  // the workspace holds whole chunks), window t's total and this chunk's prefix
-  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
-  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
-  const uint32_t tot = row[gridDim.x];  // window t's keys in the batch (k_wo_scan_rows)
-  const uint32_t pre = row[c];          // ... in the chunks before this one
-  cw[4u * t + 0] = cwv.x;
-  cw[4u * t + 1] = cwv.y;
-  cw[4u * t + 2] = cwv.z;
-  cw[4u * t + 3] = cwv.w;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    next[v][t] = 0;
-    peer_mask[v][t] = 0;
-  }
-  __syncthreads();
-  // each wave's histogram of its 1024 window bytes (next[] as counters for now)
-  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
-  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
-  uint32_t ws[kWoSub / 64];  // this lane's window in every step
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st)
-    if (s0 + 64u * st + lane < s1) atomicAdd(&next[wave][ws[st]], 1u);
-  __syncthreads();
-  // window t: its keys in the chunk (hc), in waves 0..v-1, and two exclusive scans over
-  // the 256 windows: of the totals (the window's base in perm) and of hc (its local start)
-  uint32_t hv[4], hc = 0;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    hv[v] = next[v][t];
-    hc += hv[v];
-  }
-  uint32_t it = tot, ih = hc;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
-    if (lane >= d) {
-      it += ut;
-      ih += uh;
-    }
-  }
-  if (lane == 63) {
-    tsum[0][wave] = it;
-    tsum[1][wave] = ih;
-  }
-  __syncthreads();
-  uint32_t bbase = it - tot, lbase = ih - hc;
-  for (uint32_t v = 0; v < wave; ++v) {
-    bbase += tsum[0][v];
-    lbase += tsum[1][v];
-  }
-  if (c == 0 && win_start) {
-    win_start[t] = bbase;
-    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
-  }
-  gdelta[t] = bbase + pre - lbase;
-  {
-    uint32_t run = lbase;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      next[v][t] = run;
-      run += hv[v];
-    }
-  }
-  __syncthreads();
-  // (1) the chunk's stable window order, in LDS
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-    if (s0 + 64u * st >= s1) break;  // wave-uniform
-    const uint32_t i = s0 + 64u * st + lane;
-    const uint32_t w = ws[st];
-    const bool valid = i < s1;
-    if (valid) atomicOr(reinterpret_cast<unsigned long long*>(&peer_mask[wave][w]), 1ull << lane);
-    if (valid) {
-      const uint64_t peers = peer_mask[wave][w];
-      const uint32_t base = next[wave][w];
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-      sorted[base + rank] = i | (w << 16);
-      if (rank == 0) {  // one lane per window: no conflict
-        next[wave][w] = base + (uint32_t)__popcll(peers);
-        peer_mask[wave][w] = 0;
-      }
-    }
-  }
-  __syncthreads();
-  // (2) out in that order: local position j holds key offset i of window w
-  uint32_t e[kWoChunk / kWoThreads];
-#pragma unroll
-  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) e[q] = sorted[min(t + kWoThreads * q, kn - 1u)];
-#pragma unroll
-  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
-    const uint32_t j = t + kWoThreads * q;
-    const uint32_t g = gdelta[e[q] >> 16] + j;
-    if (j < kn) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
-  }
-}
-
 // The lanes of the wave whose window byte equals this lane's (its "peers",
 // itself included): eight ballots, one per bit of the byte, each folded into
 // the lanes that differ from this one in that bit (v_bitop3: diff |= m ^ bal).
@@ -307,270 +175,33 @@ __device__ __forceinline__ uint64_t match_byte(uint32_t w) {
   return ~(((uint64_t)hi << 32) | lo);
 }
 
-// k_wo_scatter with the step's peers found by ballots instead of LDS atomics:
-// (1) each wave walks its 1024 keys, 64 per step: a lane's rank among the
-// wave's keys of its window = the window's count so far (cnt, read) + its rank
-// among the step's peers; the lowest peer advances the count (one plain read and
-// one plain write per step, no atomics); (2) per window the waves' counts become
-// their first local positions; (3) each key goes to sorted[first + rank];
-// (4) out in order, as k_wo_scatter.
-__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_ballot(const uint8_t* __restrict__ wins, uint64_t n,
-                                                                 const uint32_t* __restrict__ counts,
-                                                                 uint32_t* __restrict__ perm,
-                                                                 uint32_t* __restrict__ win_start, uint32_t dbg) {
-  __shared__ uint32_t cnt[4][kWoBins];   // per wave: the window's keys so far, then its first local position
-  __shared__ uint32_t cw[kWoChunk / 4];  // the chunk's window bytes
-  __shared__ uint32_t sorted[kWoChunk];  // the chunk's keys in window order: offset | window << 16
-  __shared__ uint32_t gdelta[kWoBins];   // window t's perm position minus its local one
-  __shared__ uint32_t tsum[2][4];
-  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
-  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
-  const uint64_t k0 = (uint64_t)c * kWoChunk;
-  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
-  u32x4 cwv = {t * 0x01010101u, 0u, 0u, 0u};
-  uint32_t tot = 4096u, pre = c * 16u;
-  if (!(dbg & 32)) {
-    cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
-    tot = row[gridDim.x];
-    pre = row[c];
-  }
-  cw[4u * t + 0] = cwv.x;
-  cw[4u * t + 1] = cwv.y;
-  cw[4u * t + 2] = cwv.z;
-  cw[4u * t + 3] = cwv.w;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
-  __syncthreads();
-  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
-  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
-  uint32_t ws[kWoSub / 64], rk[kWoSub / 64] = {};
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
-  // (1) ranks within the wave
-  if (dbg & 1) {
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) rk[st] = 64u * st + lane;
-  } else
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-    const bool valid = s0 + 64u * st + lane < s1;
-    const uint64_t peers = ((dbg & 128) ? (1ull << lane) : match_byte(ws[st])) & __builtin_amdgcn_ballot_w64(valid);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-    if (dbg & 64) {
-      rk[st] = rank + (uint32_t)__popcll(peers);
-      continue;
-    }
-    const uint32_t base = cnt[wave][ws[st]];
-    rk[st] = base + rank;
-    if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
-  }
-  __syncthreads();
-  // (2) window t: its keys in the chunk and in waves 0..v-1; exclusive scans over
-  // the windows of the totals (its base in perm) and of the chunk counts (its local start)
-  uint32_t hv[4], hc = 0;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    hv[v] = cnt[v][t];
-    hc += hv[v];
-  }
-  uint32_t it = tot, ih = hc;
-  if (!(dbg & 16))
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
-    if (lane >= d) {
-      it += ut;
-      ih += uh;
-    }
-  }
-  if (lane == 63) {
-    tsum[0][wave] = it;
-    tsum[1][wave] = ih;
-  }
-  __syncthreads();
-  uint32_t bbase = it - tot, lbase = ih - hc;
-  for (uint32_t v = 0; v < wave; ++v) {
-    bbase += tsum[0][v];
-    lbase += tsum[1][v];
-  }
-  if (c == 0 && win_start) {
-    win_start[t] = bbase;
-    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
-  }
-  gdelta[t] = bbase + pre - lbase;
-  {
-    uint32_t run = lbase;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      cnt[v][t] = (dbg & 1) ? 0u : run;
-      run += hv[v];
-    }
-  }
-  __syncthreads();
-  // (3) the chunk's stable window order, in LDS
-  if (!(dbg & 2))
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-    const uint32_t i = s0 + 64u * st + lane;
-    if (i < s1) sorted[(cnt[wave][ws[st]] + rk[st]) & 4095u] = i | (ws[st] << 16);
-  }
-  __syncthreads();
-  // (4) out in that order: local position j holds key offset i of window w
-  uint32_t e[kWoChunk / kWoThreads];
-#pragma unroll
-  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) e[q] = sorted[min(t + kWoThreads * q, kn - 1u)];
-#pragma unroll
-  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
-    const uint32_t j = t + kWoThreads * q;
-    const uint32_t g = (dbg & 4) ? (uint32_t)k0 + j : min(gdelta[(e[q] >> 16) & 255u] + j, (uint32_t)n - 1u);
-    if (j < kn && (!(dbg & 8) || e[q] == 0xffffffffu)) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
-  }
-}
-
-// k_wo_scatter with each step's ranks taken from LDS atomics that return the
-// old count (ds_add_rtn_u32: one instruction per step, no ballots): lanes of a
-// step that share a window get consecutive counts, and the stable order needs
-// them in lane order. The order is then checked where it is written out (each
-// window's run of the sorted chunk must hold increasing key offsets: with the
-// counts exact, that is exactly the stable order); a chunk that fails the
-// check is ordered again with ballots (k_wo_scatter_ballot's ranks), so the
-// result never depends on the order the LDS unit serves same-address lanes in.
-__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_fast(const uint8_t* __restrict__ wins, uint64_t n,
-                                                               const uint32_t* __restrict__ counts,
-                                                               uint32_t* __restrict__ perm,
-                                                               uint32_t* __restrict__ win_start, uint32_t dbg) {
-  __shared__ uint32_t cnt[4][kWoBins];
-  __shared__ uint32_t cw[kWoChunk / 4];
-  __shared__ uint32_t sorted[kWoChunk];
-  __shared__ uint32_t gdelta[kWoBins];
-  __shared__ uint32_t tsum[2][4];
-  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
-  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
-  const uint64_t k0 = (uint64_t)c * kWoChunk;
-  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
-  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
-  const uint32_t tot = row[gridDim.x];
-  const uint32_t pre = row[c];
-  cw[4u * t + 0] = cwv.x;
-  cw[4u * t + 1] = cwv.y;
-  cw[4u * t + 2] = cwv.z;
-  cw[4u * t + 3] = cwv.w;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
-  __syncthreads();
-  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
-  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
-  uint32_t ws[kWoSub / 64], rk[kWoSub / 64];
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = cwb[s0 + 64u * st + lane];
-  // (1) ranks within the wave: the window's count so far, one atomic per step
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st)
-    rk[st] = s0 + 64u * st + lane < s1 ? atomicAdd(&cnt[wave][ws[st]], 1u) : 0u;
-  for (int pass = 0;; ++pass) {
-    __syncthreads();
-    // (2) window t: its keys in the chunk and in waves 0..v-1; exclusive scans over
-    // the windows of the totals (its base in perm) and of the chunk counts (its local start)
-    uint32_t hv[4], hc = 0;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      hv[v] = cnt[v][t];
-      hc += hv[v];
-    }
-    uint32_t it = tot, ih = hc;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
-      if (lane >= d) {
-        it += ut;
-        ih += uh;
-      }
-    }
-    if (lane == 63) {
-      tsum[0][wave] = it;
-      tsum[1][wave] = ih;
-    }
-    __syncthreads();
-    uint32_t bbase = it - tot, lbase = ih - hc;
-    for (uint32_t v = 0; v < wave; ++v) {
-      bbase += tsum[0][v];
-      lbase += tsum[1][v];
-    }
-    if (c == 0 && win_start && pass == 0) {
-      win_start[t] = bbase;
-      if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
-    }
-    gdelta[t] = bbase + pre - lbase;
-    {
-      uint32_t run = lbase;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        cnt[v][t] = run;
-        run += hv[v];
-      }
-    }
-    __syncthreads();
-    // (3) the chunk's window order, in LDS
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-      const uint32_t i = s0 + 64u * st + lane;
-      if (i < s1) sorted[cnt[wave][ws[st]] + rk[st]] = i | (ws[st] << 16);
-    }
-    __syncthreads();
-    // the check: within each window's run, key offsets increase
-    bool bad = false;
-#pragma unroll
-    for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
-      const uint32_t j = t + kWoThreads * q;
-      if (j != 0 && j < kn) {
-        const uint32_t a = sorted[j - 1], b = sorted[j];
-        bad |= (a >> 16) == (b >> 16) && (a & 0xffffu) > (b & 0xffffu);
-      }
-    }
-    if (!__syncthreads_or((int)bad) || pass == 1 || (dbg & 1)) break;
-    // fallback: ranks from ballots (as k_wo_scatter_ballot), counts rebuilt from zero
-#pragma unroll
-    for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-      const bool valid = s0 + 64u * st + lane < s1;
-      const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-      const uint32_t base = cnt[wave][ws[st]];
-      rk[st] = base + rank;
-      if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
-    }
-  }
-  // (4) out in that order: local position j holds key offset i of window w
-  uint32_t e[kWoChunk / kWoThreads];
-#pragma unroll
-  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) e[q] = sorted[min(t + kWoThreads * q, kn - 1u)];
-#pragma unroll
-  for (uint32_t q = 0; q < kWoChunk / kWoThreads; ++q) {
-    const uint32_t j = t + kWoThreads * q;
-    const uint32_t g = gdelta[e[q] >> 16] + j;
-    if (j < kn) perm[g] = (uint32_t)(k0 + (e[q] & 0xffffu));
-  }
-}
-
-// LDS-lean forms of k_wo_scatter_ballot (more workgroups per CU):
-//   V = 1: no LDS copy of the window bytes (each lane loads its 16 bytes, one per
-//          step, from the workspace), sorted entries u32 (offset | window << 16);
-//   V = 2: the window bytes in LDS, sorted entries u16 (the offset; the output
-//          pass reads the key's window back from the bytes).
-template <int V>
-__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_v(const uint8_t* __restrict__ wins, uint64_t n,
+// One chunk per workgroup. (1) Each wave walks its 1024 keys in key order, 64
+// per step: a lane's rank among the wave's keys of its window = the window's
+// count so far (cnt, one plain LDS read) + its rank among the step's peers
+// (match_byte: eight ballots); the lowest peer advances the count (one plain
+// write; LDS accesses of a wave execute in order, so the next step reads it).
+// (2) Per window (thread t = window t): the waves' counts become each wave's
+// first local position (exclusive scans over the windows of the chunk counts
+// and of the batch totals, and over the waves); gdelta = the window's perm
+// position minus its local one (its base from the totals + the chunk's prefix,
+// k_wo_scan_rows). (3) Each key's offset goes to sorted[first + rank] (u16).
+// (4) The chunk leaves in that order, thread t the positions t, t + 256, ...:
+// a window's keys are consecutive both in LDS and in perm, so each store
+// instruction writes a few runs of whole lines. Measured against other forms
+// per 10M keys (profiles/r4/win_order/README.md): 64-bit LDS peer masks with
+// atomic OR and u32 entries (round 3) 26 us; ballots, u32 entries 25; this
+// (ballots, u16 entries: 17 KiB of LDS, 7 workgroups per CU) 23; one ordering
+// pass after per-wave histograms 24; persistent workgroups prefetching the
+// next chunk 28-42; ranks from LDS atomics with return (served in lane order in
+// every test, checked) 69.
+__global__ __launch_bounds__(kWoThreads) void k_wo_scatter(const uint8_t* __restrict__ wins, uint64_t n,
                                                             const uint32_t* __restrict__ counts,
                                                             uint32_t* __restrict__ perm,
                                                             uint32_t* __restrict__ win_start) {
-  __shared__ uint32_t cnt[4][kWoBins];
-  __shared__ uint32_t cw[V == 2 ? kWoChunk / 4 : 1];
-  __shared__ uint32_t sorted32[V == 1 ? kWoChunk : 1];
-  __shared__ uint16_t sorted16[V == 2 ? kWoChunk : 1];
-  __shared__ uint32_t gdelta[kWoBins];
+  __shared__ uint32_t cnt[4][kWoBins];          // per wave: the window's keys so far, then its first position
+  __shared__ uint32_t cw[kWoChunk / 4];         // the chunk's window bytes
+  __shared__ uint16_t sorted[kWoChunk];         // the chunk's key offsets in window order
+  __shared__ uint32_t gdelta[kWoBins];          // window t's perm position minus its local one
   __shared__ uint32_t tsum[2][4];
   const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
   const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
@@ -580,12 +211,9 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_v(const uint8_t* __re
   const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
   const uint32_t tot = row[gridDim.x];
   const uint32_t pre = row[c];
-  uint32_t ws[kWoSub / 64];
-  if constexpr (V == 1) {
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = wins[k0 + s0 + 64u * st + lane];
-  } else {
-    const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
+  uint32_t ws[kWoSub / 64];  // this lane's window in every step
+  {
+    const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);  // the workspace holds whole chunks
     cw[4u * t + 0] = cwv.x;
     cw[4u * t + 1] = cwv.y;
     cw[4u * t + 2] = cwv.z;
@@ -598,7 +226,7 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_v(const uint8_t* __re
   uint32_t rk[kWoSub / 64];
 #pragma unroll
   for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-    if constexpr (V == 2) ws[st] = cwb[s0 + 64u * st + lane];
+    ws[st] = cwb[s0 + 64u * st + lane];
     const bool valid = s0 + 64u * st + lane < s1;
     const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
@@ -649,11 +277,8 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_v(const uint8_t* __re
 #pragma unroll
   for (uint32_t st = 0; st < kWoSub / 64; ++st) {
     const uint32_t i = s0 + 64u * st + lane;
-    if constexpr (V == 2) ws[st] = cwb[i];  // read again: not held across the barriers
-    if (i < s1) {
-      if constexpr (V == 1) sorted32[cnt[wave][ws[st]] + rk[st]] = i | (ws[st] << 16);
-      else sorted16[cnt[wave][ws[st]] + rk[st]] = (uint16_t)i;
-    }
+    ws[st] = cwb[i];  // read again: not held across the barriers
+    if (i < s1) sorted[cnt[wave][ws[st]] + rk[st]] = (uint16_t)i;
   }
   __syncthreads();
 #pragma unroll
@@ -662,235 +287,15 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_scatter_v(const uint8_t* __re
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
       const uint32_t j = min(t + kWoThreads * (q0 + q), kn - 1u);
-      if constexpr (V == 1) e[q] = sorted32[j];
-      else e[q] = sorted16[j];
+      e[q] = sorted[j];
     }
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
       const uint32_t j = t + kWoThreads * (q0 + q);
-      const uint32_t w = V == 1 ? (e[q] >> 16) : (uint32_t)cwb[e[q]];
-      if (j < kn) perm[gdelta[w] + j] = (uint32_t)(k0 + (e[q] & 0xffffu));
+      const uint32_t w = cwb[e[q]];
+      if (j < kn) perm[gdelta[w] + j] = (uint32_t)(k0 + e[q]);
     }
     asm volatile("" ::: "memory");
-  }
-}
-
-// k_wo_scatter_ballot in one ordering pass: the waves' histograms first (LDS
-// adds, no return), so every wave's count per window starts at that window's
-// first local position for the wave; each step then places its keys directly
-// (base + rank among the step's peers) and the lowest peer advances the count.
-// Fewer LDS accesses at random addresses per key (about 4 instead of 5) and no
-// ranks held across barriers.
-__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_one(const uint8_t* __restrict__ wins, uint64_t n,
-                                                              const uint32_t* __restrict__ counts,
-                                                              uint32_t* __restrict__ perm,
-                                                              uint32_t* __restrict__ win_start) {
-  __shared__ uint32_t cnt[4][kWoBins];
-  __shared__ uint32_t cw[kWoChunk / 4];
-  __shared__ uint32_t sorted[kWoChunk];
-  __shared__ uint32_t gdelta[kWoBins];
-  __shared__ uint32_t tsum[2][4];
-  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
-  const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
-  const uint64_t k0 = (uint64_t)c * kWoChunk;
-  const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
-  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
-  const uint32_t tot = row[gridDim.x];
-  const uint32_t pre = row[c];
-  const u32x4 cwv = *reinterpret_cast<const u32x4*>(wins + k0 + 16u * t);
-  cw[4u * t + 0] = cwv.x;
-  cw[4u * t + 1] = cwv.y;
-  cw[4u * t + 2] = cwv.z;
-  cw[4u * t + 3] = cwv.w;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
-  __syncthreads();
-  const uint8_t* cwb = reinterpret_cast<const uint8_t*>(cw);
-  // the wave's histogram of its 1024 window bytes
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-    const uint32_t i = s0 + 64u * st + lane;
-    if (i < s1) atomicAdd(&cnt[wave][cwb[i]], 1u);
-  }
-  __syncthreads();
-  uint32_t hv[4], hc = 0;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    hv[v] = cnt[v][t];
-    hc += hv[v];
-  }
-  uint32_t it = tot, ih = hc;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
-    if (lane >= d) {
-      it += ut;
-      ih += uh;
-    }
-  }
-  if (lane == 63) {
-    tsum[0][wave] = it;
-    tsum[1][wave] = ih;
-  }
-  __syncthreads();
-  uint32_t bbase = it - tot, lbase = ih - hc;
-  for (uint32_t v = 0; v < wave; ++v) {
-    bbase += tsum[0][v];
-    lbase += tsum[1][v];
-  }
-  if (c == 0 && win_start) {
-    win_start[t] = bbase;
-    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
-  }
-  gdelta[t] = bbase + pre - lbase;
-  {
-    uint32_t run = lbase;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      cnt[v][t] = run;
-      run += hv[v];
-    }
-  }
-  __syncthreads();
-  // each step's keys straight to their local positions
-#pragma unroll
-  for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-    const uint32_t i = s0 + 64u * st + lane;
-    const uint32_t w = cwb[i];
-    const bool valid = i < s1;
-    const uint64_t peers = match_byte(w) & __builtin_amdgcn_ballot_w64(valid);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-    const uint32_t base = cnt[wave][w];
-    if (valid) sorted[base + rank] = i | (w << 16);
-    if (valid && rank == 0) cnt[wave][w] = base + (uint32_t)__popcll(peers);
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t q0 = 0; q0 < kWoChunk / kWoThreads; q0 += 8) {
-    uint32_t e[8];
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) e[q] = sorted[min(t + kWoThreads * (q0 + q), kn - 1u)];
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) {
-      const uint32_t j = t + kWoThreads * (q0 + q);
-      if (j < kn) perm[gdelta[e[q] >> 16] + j] = (uint32_t)(k0 + (e[q] & 0xffffu));
-    }
-  }
-}
-
-// Persistent variant of k_wo_scatter_ballot: gridDim.x workgroups (a multiple
-// of 8), workgroup g on XCD g % 8 walks that XCD's contiguous range of chunks
-// with a stride of the XCD's workgroups, and loads the next chunk's window bytes
-// and prefixes before ordering the current one (the loads of a chunk are a
-// latency the order of the previous one hides). A lane reads its own 16
-// window bytes (one per step) straight from the workspace: no LDS copy.
-__global__ __launch_bounds__(kWoThreads) void k_wo_scatter_pf(const uint8_t* __restrict__ wins, uint64_t n,
-                                                             uint32_t chunks, const uint32_t* __restrict__ counts,
-                                                             uint32_t* __restrict__ perm,
-                                                             uint32_t* __restrict__ win_start, uint32_t dbg) {
-  __shared__ uint32_t cnt[4][kWoBins];
-  __shared__ uint32_t sorted[kWoChunk];
-  __shared__ uint32_t gdelta[kWoBins];
-  __shared__ uint32_t tsum[2][4];
-  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
-  const uint32_t G = gridDim.x, x = blockIdx.x % 8u, gi = blockIdx.x / 8u, P = G / 8u;
-  const uint32_t q = chunks / 8u, r8 = chunks % 8u;
-  const uint32_t xc0 = x * q + min(x, r8), xc1 = xc0 + q + (x < r8 ? 1u : 0u);  // this XCD's chunks
-  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(chunks);
-  const uint32_t tot = row[chunks];
-  uint32_t c = xc0 + gi;
-  uint32_t nws[kWoSub / 64], npre = 0;
-  auto fetch = [&](uint32_t cc) {
-    const uint64_t kb = (uint64_t)cc * kWoChunk + kWoSub * wave + lane;
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) nws[st] = wins[kb + 64u * st];
-    npre = row[cc];
-  };
-  if (c < xc1) fetch(c);
-  for (; c < xc1; c += P) {
-    uint32_t ws[kWoSub / 64];
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) ws[st] = nws[st];
-    const uint32_t pre = npre;
-    if (c + P < xc1) fetch(c + P);
-    const uint64_t k0 = (uint64_t)c * kWoChunk;
-    const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) cnt[v][t] = 0;
-    __syncthreads();
-    const uint32_t s0 = kWoSub * wave, s1 = min(kn, s0 + kWoSub);
-    uint32_t rk[kWoSub / 64];
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-      if (dbg & 1) {
-        rk[st] = 64u * st + lane;
-        continue;
-      }
-      const bool valid = s0 + 64u * st + lane < s1;
-      const uint64_t peers = match_byte(ws[st]) & __builtin_amdgcn_ballot_w64(valid);
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-      const uint32_t base = cnt[wave][ws[st]];
-      rk[st] = base + rank;
-      if (valid && rank == 0) cnt[wave][ws[st]] = base + (uint32_t)__popcll(peers);
-    }
-    __syncthreads();
-    uint32_t hv[4], hc = 0;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      hv[v] = cnt[v][t];
-      hc += hv[v];
-    }
-    uint32_t it = tot, ih = hc;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
-      if (lane >= d) {
-        it += ut;
-        ih += uh;
-      }
-    }
-    if (lane == 63) {
-      tsum[0][wave] = it;
-      tsum[1][wave] = ih;
-    }
-    __syncthreads();
-    uint32_t bbase = it - tot, lbase = ih - hc;
-    for (uint32_t v = 0; v < wave; ++v) {
-      bbase += tsum[0][v];
-      lbase += tsum[1][v];
-    }
-    if (c == 0 && win_start) {
-      win_start[t] = bbase;
-      if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
-    }
-    gdelta[t] = bbase + pre - lbase;
-    {
-      uint32_t run = lbase;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        cnt[v][t] = (dbg & 1) ? 0u : run;
-        run += hv[v];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t st = 0; st < kWoSub / 64; ++st) {
-      const uint32_t i = s0 + 64u * st + lane;
-      if (i < s1) sorted[(dbg & 1) ? i : cnt[wave][ws[st]] + rk[st]] = i | (ws[st] << 16);
-    }
-    __syncthreads();
-    uint32_t e[kWoChunk / kWoThreads];
-#pragma unroll
-    for (uint32_t qq = 0; qq < kWoChunk / kWoThreads; ++qq) e[qq] = sorted[min(t + kWoThreads * qq, kn - 1u)];
-#pragma unroll
-    for (uint32_t qq = 0; qq < kWoChunk / kWoThreads; ++qq) {
-      const uint32_t j = t + kWoThreads * qq;
-      const uint32_t g = (dbg & 4) ? (uint32_t)k0 + j : min(gdelta[(e[qq] >> 16) & 255u] + j, (uint32_t)n - 1u);
-      if (j < kn) perm[g] = (uint32_t)(k0 + (e[qq] & 0xffffu));
-    }
-    // the next chunk's first LDS writes (cnt) follow every wave's reads of this one's
-    __syncthreads();
   }
 }
 
@@ -924,27 +329,7 @@ hipError_t launch_win_order_bytes(uint64_t n, bool hist_done, uint32_t* perm, ui
   const uint8_t* wins = win_order_wins(workspace, n);
   if (!hist_done) hipLaunchKernelGGL(k_wo_hist_bytes, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts);
   hipLaunchKernelGGL(k_wo_scan_rows, dim3(kWoBins), dim3(256), 0, st, counts, chunks);
-  const char* e = getenv("SHF_HB_WO_SCATTER");  // EXPERIMENT (removed once a variant is chosen)
-  if (e && e[0] == '2')
-    hipLaunchKernelGGL(k_wo_scatter_ballot, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start,
-                       (uint32_t)atoi(e + 1));
-  else if (e && e[0] == '5' && e[1] == '1')
-    hipLaunchKernelGGL(k_wo_scatter_v<1>, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
-  else if (e && e[0] == '5' && e[1] == '2')
-    hipLaunchKernelGGL(k_wo_scatter_v<2>, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
-  else if (e && e[0] == '6')
-    hipLaunchKernelGGL(k_wo_scatter_one, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
-  else if (e && e[0] == '4')
-    hipLaunchKernelGGL(k_wo_scatter_fast, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start,
-                       (uint32_t)atoi(e + 1));
-  else if (e && e[0] == '3') {  // 3<wgs per CU><dbg>
-    const uint32_t per_cu = (uint32_t)(e[1] - '0');
-    const uint32_t g = std::min<uint32_t>((chunks + 7u) / 8u * 8u, 256u * per_cu);
-    hipLaunchKernelGGL(k_wo_scatter_pf, dim3(g), dim3(kWoThreads), 0, st, wins, n, chunks, counts, perm, win_start,
-                       (uint32_t)atoi(e + 2));
-  }
-  else
-    hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
+  hipLaunchKernelGGL(k_wo_scatter, dim3(chunks), dim3(kWoThreads), 0, st, wins, n, counts, perm, win_start);
   return hipGetLastError();
 }
 
