@@ -82,8 +82,8 @@ KERNEL_SYMS = {"fixed16": "k_fixed16<0>", "fixed16_hot": "k_fixed16<0>", "shard1
                "winorder": "k_wo_", "hashwin16": "k_fixed16_win"}
 # workloads whose one call is several kernels: their counters are summed over the kernels
 # (each kernel's median per launch), so traffic covers the whole call
-MULTI_KERNEL = {"winorder": ["k_wo_hist", "k_wo_scan_rows", "k_wo_scatter"],
-                "hashwin16": ["k_fixed16_win", "k_wo_scan_rows", "k_wo_scatter"]}
+MULTI_KERNEL = {"winorder": ["k_wo_rank", "k_wo_scan_rows", "k_wo_place"],
+                "hashwin16": ["k_fixed16_win", "k_wo_scan_rows", "k_wo_place"]}
 HASH_WORKLOADS = ["fixed16", "fixed16_hot", "shard1b", "fixed256", "var", "probe16", "probe16_hbm", "tabpart",
                   "winorder", "hashwin16"]
 CEIL_WORKLOADS = ["ceil_copy", "ceil_copynt", "ceil_copy_hot", "ceil_copynt_hot", "ceil_copy_1b", "ceil_copynt_1b",
@@ -328,7 +328,7 @@ def grid_threads(name, n):
     if name == "tabpart":
         return n * 512                  # k_tab_split: one 512-thread workgroup per tab
     if name in ("winorder", "hashwin16"):
-        return (n + 4095) // 4096 * 256  # k_wo_scatter (and k_fixed16_win): one 256-thread workgroup per 4096 keys
+        return (n + 4095) // 4096 * 256  # k_wo_place (and k_wo_rank): one 256-thread workgroup per 4096 keys
     return None
 
 
@@ -666,7 +666,7 @@ def win_order_workload(args, dev, seed_base):
               np.array_equal(start.cpu().numpy().view(np.uint32), want_s))
         return bool(ok), int(n)
 
-    return Workload("winorder", n, 16 + 4, [launch], "k_wo_hist + k_wo_scan_rows + k_wo_scatter",
+    return Workload("winorder", n, 16 + 4, [launch], "k_wo_rank + k_wo_scan_rows + k_wo_place",
                     "%d 16-B hash records ordered by window (stable counting sort, 3 launches)" % n, verify,
                     grid_threads("winorder", n))
 
@@ -715,7 +715,7 @@ def hash_win_workload(args, dev, pairs):
             checked += n
         return bool(ok), int(checked)
 
-    w = Workload("hashwin16", n, 16 + 16 + 4, launches, "k_fixed16_win + k_wo_scan_rows + k_wo_scatter",
+    w = Workload("hashwin16", n, 16 + 16 + 4, launches, "k_fixed16_win + k_wo_scan_rows + k_wo_place",
                  "%d 16-B keys hashed and window-ordered in one call (records + perm), rotating over %d batches"
                  % (n, len(pairs)), verify, grid_threads("hashwin16", n))
     w.keep = bufs

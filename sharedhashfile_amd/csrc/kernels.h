@@ -34,7 +34,8 @@ struct Sink {
   const uint32_t* win_tab = nullptr;
   uint32_t* status = nullptr;  // variable-length keys: set to 1 when a key's offsets are invalid
   uint8_t* wins = nullptr;     // kOutHashWin: n window bytes (rounded up to whole kWoChunk chunks)
-  uint32_t* win_counts = nullptr;  // kOutHashWin, fused 16-B kernel: each chunk's 256-bin histogram
+  uint32_t* win_counts = nullptr;  // kOutHashWin, fused 16-B kernel: each chunk's 256 window counts
+  uint16_t* win_sorted = nullptr;  // kOutHashWin, fused 16-B kernel: each chunk's order by window (win_rank.h)
 };
 
 // Window-order geometry, shared by the hashing kernels' fused epilogue and the
@@ -90,16 +91,18 @@ hipError_t launch_tab_split(const void* src, uint64_t src_bytes, void* dst, uint
 uint64_t win_order_workspace_bytes(uint64_t n);
 hipError_t launch_win_order(const void* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, void* workspace,
                             hipStream_t st);
-// The workspace's window bytes and counts rows, for a hashing launch with
-// kOutHashWin to fill; then launch_win_order_bytes orders from them (counting
-// the chunks itself unless the hashing kernel did: hist_done).
+// The workspace's window bytes, counts rows and chunk orders, for a hashing
+// launch with kOutHashWin to fill; then launch_win_order_bytes orders from them
+// (ranking the chunks' window bytes itself unless the hashing kernel ranked
+// them: ranked).
 uint8_t* win_order_wins(void* workspace, uint64_t n);
 uint32_t* win_order_counts(void* workspace);
-hipError_t launch_win_order_bytes(uint64_t n, bool hist_done, uint32_t* perm, uint32_t* win_start, void* workspace,
+uint16_t* win_order_sorted(void* workspace, uint64_t n);
+hipError_t launch_win_order_bytes(uint64_t n, bool ranked, uint32_t* perm, uint32_t* win_start, void* workspace,
                                   hipStream_t st);
 // Fixed-length hash + window bytes (kOutHashWin): 16-B keys go through the fused
-// kernel, which also writes the chunk histograms (*hist_done = true).
+// kernel, which ranks each chunk itself (win_counts, win_sorted; *ranked = true).
 hipError_t launch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
-                            hipStream_t st, int kernel, bool* hist_done);
+                            hipStream_t st, int kernel, bool* ranked);
 
 }  // namespace shfhb

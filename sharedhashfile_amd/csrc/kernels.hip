@@ -34,6 +34,7 @@
 
 #include "murmur3_mix.h"
 #include "kernels.h"
+#include "win_rank.h"
 
 namespace shfhb {
 
@@ -254,50 +255,46 @@ __global__ __launch_bounds__(kF16Block) void k_fixed16(const u32x4* __restrict__
   store_result<OUT>(sink, i, s);
 }
 
-// 16-B keys hashed and counted for the window order in one pass (kOutHashWin):
-// one workgroup per kWoChunk-key chunk, kWoChunk / BLOCK keys per lane
-// (lane t takes keys BLOCK j + t, so each load instruction reads BLOCK x 16 B of
-// consecutive keys; all of them in flight before the first is hashed). Beside
-// each hash record it writes the key's window byte and the chunk's 256-bin
-// histogram (LDS atomics, into the bin-major counts): the order passes then
-// never read the 16-B records back (win_order.hip).
-// 1024 threads (4 keys per lane): 256 threads (16 keys per lane) 63 us per 10M
-// keys, 512 60, 1024 59 (k_fixed16 alone 51; profiles/r4/win_order/README.md).
+// 16-B keys hashed and ranked for the window order in one pass (kOutHashWin):
+// one workgroup per kWoChunk-key chunk, kWoChunk / BLOCK keys per lane (wave v
+// owns keys [v * 64 kKpl, (v + 1) * 64 kKpl), 64 consecutive records per load
+// instruction; all of a lane's loads in flight before the first key is hashed).
+// Beside each hash record it ranks the chunk by window (win_rank.h: ballots,
+// per-wave counts and scans in LDS -- VALU and LDS work this HBM-bound kernel
+// has room for) and writes the chunk's 256 window counts and its order (4096
+// u16 offsets): the order passes then never read the 16-B records back, and the
+// placement after the scan is one load and one store per key (win_order.hip).
 constexpr uint32_t kF16WinBlock = 1024;
 
 template <uint32_t BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_fixed16_win(const u32x4* __restrict__ keys, uint64_t n, uint32_t seed,
                                                        Sink sink) {
-  constexpr uint32_t kKpl = kWoChunk / BLOCK;
-  __shared__ uint32_t hist[kWoBins];
-  __shared__ __attribute__((aligned(16))) uint8_t cwb[kWoChunk];
-  const uint32_t t = threadIdx.x;
+  constexpr uint32_t kKpl = kWoChunk / BLOCK, kWaves = BLOCK / 64u;
+  __shared__ WoRankLds<kWaves> L;
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63u;
   const uint32_t c = xcd_major(blockIdx.x, gridDim.x);
   const uint64_t k0 = (uint64_t)c * kWoChunk;
   const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
-  if (t < kWoBins) hist[t] = 0;
-  u32x4 k[kKpl];  // past the batch: the last key again (hashed, neither stored nor counted)
+  wo_rank_init(L);
+  u32x4 k[kKpl];  // past the batch: the last key again (hashed, neither stored nor ranked)
 #pragma unroll
-  for (uint32_t j = 0; j < kKpl; ++j) k[j] = __builtin_nontemporal_load(&keys[k0 + min(BLOCK * j + t, kn - 1u)]);
-  __syncthreads();
+  for (uint32_t j = 0; j < kKpl; ++j)
+    k[j] = __builtin_nontemporal_load(&keys[k0 + min(wo_key_of<kKpl>(wave, j, lane), kn - 1u)]);
+  uint32_t w[kKpl];
 #pragma unroll
   for (uint32_t j = 0; j < kKpl; ++j) {
-    const uint32_t i = BLOCK * j + t;
+    const uint32_t i = wo_key_of<kKpl>(wave, j, lane);
     State s{seed, seed};
     body_block(s, pack64(k[j].x, k[j].y), pack64(k[j].z, k[j].w));
     finish(s, 16);
-    const uint32_t w = (uint32_t)s.h1 & 0xffu;
+    w[j] = (uint32_t)s.h1 & 0xffu;  // the window, shf.c:800
     if (i < kn) {
       const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
       __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + k0 + i);
-      atomicAdd(&hist[w], 1u);
     }
-    cwb[i] = (uint8_t)w;
   }
   __syncthreads();
-  if (t < kWoBins) sink.win_counts[(uint64_t)t * wo_row_stride(gridDim.x) + c] = hist[t];
-  // the chunk's window bytes, 16 per thread (the workspace holds whole chunks)
-  if (t < kWoChunk / 16u) reinterpret_cast<u32x4*>(sink.wins + k0)[t] = reinterpret_cast<const u32x4*>(cwb)[t];
+  wo_rank_chunk<kWaves, kKpl>(w, kn, L, sink.win_counts + c, wo_row_stride(gridDim.x), sink.win_sorted + k0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1281,8 +1278,8 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
     case kOutUid:
       return launch_fixed_t<kOutUid>(keys, key_len, n, seed, sink, st, kernel);
     case kOutHashWin: {
-      bool hist_done = false;
-      return launch_fixed_win(keys, key_len, n, seed, sink, st, kernel, &hist_done);
+      bool ranked = false;
+      return launch_fixed_win(keys, key_len, n, seed, sink, st, kernel, &ranked);
     }
     default:
       return launch_fixed_t<kOutProbe>(keys, key_len, n, seed, sink, st, kernel);
@@ -1290,16 +1287,17 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
 }
 
 hipError_t launch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, const Sink& sink,
-                            hipStream_t st, int kernel, bool* hist_done) {
-  *hist_done = false;
+                            hipStream_t st, int kernel, bool* ranked) {
+  *ranked = false;
   if (n == 0) return hipSuccess;
   const bool al16 = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
-  if (key_len == 16 && al16 && sink.win_counts && (kernel == kKernelAuto || kernel == kKernelFixed16)) {
+  if (key_len == 16 && al16 && sink.win_counts && sink.win_sorted &&
+      (kernel == kKernelAuto || kernel == kKernelFixed16)) {
     const uint64_t chunks = (n + kWoChunk - 1) / kWoChunk;
     if (chunks > 0x7fffffffull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_fixed16_win<kF16WinBlock>, dim3((unsigned)chunks), dim3(kF16WinBlock), 0, st,
                        reinterpret_cast<const u32x4*>(keys), n, seed, sink);
-    *hist_done = true;
+    *ranked = true;
     return hipGetLastError();
   }
   return launch_fixed_t<kOutHashWin>(keys, key_len, n, seed, sink, st, kernel);

@@ -1120,14 +1120,15 @@ int shf_hash_batch_fixed_win_kernel_async(const void* d_keys, uint32_t key_len, 
   int rc = current_ctx(&c);
   if (rc) return rc;
   const hipStream_t st = (hipStream_t)hip_stream;
-  bool hist_done = false;
+  bool ranked = false;
   if (n) {
     shfhb::Sink k = out_sink(d_out);
     k.wins = shfhb::win_order_wins(d_workspace, n);
     k.win_counts = shfhb::win_order_counts(d_workspace);
-    HB_TRY(shfhb::launch_fixed_win(d_keys, key_len, n, seed, k, st, kernel, &hist_done));
+    k.win_sorted = shfhb::win_order_sorted(d_workspace, n);
+    HB_TRY(shfhb::launch_fixed_win(d_keys, key_len, n, seed, k, st, kernel, &ranked));
   }
-  HB_TRY(shfhb::launch_win_order_bytes(n, hist_done, d_perm, d_win_start, d_workspace, st));
+  HB_TRY(shfhb::launch_win_order_bytes(n, ranked, d_perm, d_win_start, d_workspace, st));
   return SHF_HB_OK;
 }
 
@@ -1191,7 +1192,7 @@ int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t 
   const hipStream_t st = c->st[0];
   if (mem == SHF_HASH_MEM_DEVICE) {
     shfhb::Sink k = out_sink(out);
-    bool hist_done = false;
+    bool ranked = false;
     if (n) {
       k.wins = shfhb::win_order_wins(ws, n);
       if (var) {
@@ -1200,10 +1201,11 @@ int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t 
         HB_TRY(shfhb::launch_var(keys, offsets, 0, n, seed, k, shfhb::kOutHashWin, st));
       } else {
         k.win_counts = shfhb::win_order_counts(ws);
-        HB_TRY(shfhb::launch_fixed_win(keys, key_len, n, seed, k, st, shfhb::kKernelAuto, &hist_done));
+        k.win_sorted = shfhb::win_order_sorted(ws, n);
+        HB_TRY(shfhb::launch_fixed_win(keys, key_len, n, seed, k, st, shfhb::kKernelAuto, &ranked));
       }
     }
-    HB_TRY(shfhb::launch_win_order_bytes(n, hist_done, perm, win_start, ws, st));
+    HB_TRY(shfhb::launch_win_order_bytes(n, ranked, perm, win_start, ws, st));
     if (var && n) HB_TRY(hipMemcpyAsync(c->h_status, k.status, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HB_TRY(hipStreamSynchronize(st));
     return var && n && *c->h_status ? SHF_HB_ERR_ARG : SHF_HB_OK;

@@ -177,7 +177,7 @@ def test_line_for_eight_ranks_carries_per_rank_fields():
 
 def test_multi_kernel_workload_counters_sum_over_its_kernels():
     rows = []
-    for k, grid, fetch in (("k_wo_hist", 625152, 100.0), ("k_wo_scan_rows", 65536, 10.0), ("k_wo_scatter", 625152, 5.0)):
+    for k, grid, fetch in (("k_wo_rank", 625152, 100.0), ("k_wo_scan_rows", 65536, 10.0), ("k_wo_place", 625152, 5.0)):
         for rep in range(3):
             rows.append({"Kernel_Name": "void shfhb::(anonymous namespace)::%s(...)" % k, "Grid_Size": str(grid),
                          "Counter_Name": "FETCH_SIZE", "Counter_Value": str(fetch + rep)})
@@ -251,9 +251,9 @@ def test_shared_order_kernels_go_to_the_workload_that_ran_them():
     """winorder and hashwin16 share the scan and scatter kernels (same grids):
     each row goes to the workload whose own first kernel was dispatched last."""
     rows, d = [], 0
-    for first, scan_val in (("k_wo_hist", 1.0), ("k_fixed16_win", 7.0)):
+    for first, scan_val in (("k_wo_rank", 1.0), ("k_fixed16_win", 7.0)):
         for rep in range(2):
-            for k, v in ((first, 100.0), ("k_wo_scan_rows", scan_val), ("k_wo_scatter", scan_val * 10)):
+            for k, v in ((first, 100.0), ("k_wo_scan_rows", scan_val), ("k_wo_place", scan_val * 10)):
                 d += 1
                 rows.append({"Kernel_Name": "void shfhb::(anonymous namespace)::%s(...)" % k, "Grid_Size": "625152",
                              "Counter_Name": "FETCH_SIZE", "Counter_Value": str(v), "Dispatch_Id": str(d)})
