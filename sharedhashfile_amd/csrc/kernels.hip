@@ -293,7 +293,6 @@ __global__ __launch_bounds__(BLOCK) void k_fixed16_win(const u32x4* __restrict__
       __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + k0 + i);
     }
   }
-  __syncthreads();
   wo_rank_chunk<kWaves, kKpl>(w, kn, L, sink.win_counts + c, wo_row_stride(gridDim.x), sink.win_sorted + k0);
 }
 

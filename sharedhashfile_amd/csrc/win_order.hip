@@ -57,7 +57,6 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_rank(const u32x4* __restrict_
 #pragma unroll
   for (uint32_t q = 0; q < kWoSteps; ++q)
     w[q] = __builtin_nontemporal_load(&hashes[k0 + min(wo_key_of<kWoSteps>(wave, q, lane), kn - 1u)]).x & 0xffu;
-  __syncthreads();
   wo_rank_chunk<kWoThreads / 64, kWoSteps>(w, kn, L, counts + c, wo_row_stride(gridDim.x), sorted + k0);
 }
 
@@ -76,7 +75,6 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_rank_bytes(const uint8_t* __r
   uint32_t w[kWoSteps];
 #pragma unroll
   for (uint32_t q = 0; q < kWoSteps; ++q) w[q] = __builtin_nontemporal_load(&wins[k0 + wo_key_of<kWoSteps>(wave, q, lane)]);
-  __syncthreads();
   wo_rank_chunk<kWoThreads / 64, kWoSteps>(w, kn, L, counts + c, wo_row_stride(gridDim.x), sorted + k0);
 }
 
@@ -104,12 +102,7 @@ __global__ __launch_bounds__(256) void k_wo_scan_rows(uint32_t* __restrict__ cou
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) sum += v[j];
-    uint32_t inc = sum;  // inclusive scan of the threads' sums over the wave
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)inc, d);
-      if (lane >= d) inc += u;
-    }
+    const uint32_t inc = wo_wave_incl_scan(sum);  // inclusive scan of the threads' sums over the wave
     if (lane == 63) wsum[wave] = inc;
     __syncthreads();
     uint32_t run = carry + inc - sum, block = 0;
@@ -166,15 +159,7 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_place(const uint16_t* __restr
   const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
   const uint32_t tot = row[gridDim.x], pre = row[c];
   const uint32_t hc = row[c + 1] - pre;  // entry [chunks] is the total: the last chunk's difference holds too
-  uint32_t it = tot, ih = hc;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t ut = (uint32_t)__shfl_up((int)it, d), uh = (uint32_t)__shfl_up((int)ih, d);
-    if (lane >= d) {
-      it += ut;
-      ih += uh;
-    }
-  }
+  const uint32_t it = wo_wave_incl_scan(tot), ih = wo_wave_incl_scan(hc);
   if (lane == 63) {
     tsum[0][wave] = it;
     tsum[1][wave] = ih;

@@ -30,6 +30,19 @@ __device__ __forceinline__ uint64_t wo_match_byte(uint32_t w) {
   return ~(((uint64_t)hi << 32) | lo);
 }
 
+// Wave-wide inclusive scan of a u32 (DPP: shifts by 1, 2, 4, 8 lanes within
+// each row of 16, then rows 0 and 1's last lanes added into the rows after
+// them): six dependent VALU adds instead of six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wo_wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
 // LDS of one chunk's ranking in a workgroup of WAVES waves.
 template <uint32_t WAVES>
 struct WoRankLds {
@@ -38,9 +51,13 @@ struct WoRankLds {
   uint32_t tsum[4];
 };
 
+// Each wave clears its own counts (only it touches them until the barrier
+// after the ranking loop, so no barrier is needed before it).
 template <uint32_t WAVES>
 __device__ __forceinline__ void wo_rank_init(WoRankLds<WAVES>& L) {
-  for (uint32_t e = threadIdx.x; e < WAVES * kWoBins; e += WAVES * 64u) (&L.cnt[0][0])[e] = 0;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t e = lane; e < kWoBins; e += 64u) L.cnt[wave][e] = 0;
 }
 
 // Key offset in the chunk of wave `wave`'s lane `lane` at step q: each wave
@@ -62,7 +79,8 @@ __device__ __forceinline__ uint32_t wo_key_of(uint32_t wave, uint32_t q, uint32_
 // the windows and over the waves). (3) Each key's offset goes to
 // sorted[first + rank]; (4) the 8-KiB order leaves as 16 B per thread into
 // sorted_out[0, 4096) (positions >= kn hold no key). Every thread of the
-// workgroup calls it; wo_rank_init(L) and a barrier come before.
+// workgroup calls it, each wave after its own wo_rank_init(L) (no barrier
+// between); a workgroup that reuses L passes a barrier after the last call.
 template <uint32_t WAVES, uint32_t STEPS>
 __device__ __forceinline__ void wo_rank_chunk(const uint32_t (&w)[STEPS], uint32_t kn, WoRankLds<WAVES>& L,
                                               uint32_t* __restrict__ counts_col, uint64_t stride,
@@ -80,17 +98,15 @@ __device__ __forceinline__ void wo_rank_chunk(const uint32_t (&w)[STEPS], uint32
     if (valid && rank == 0) L.cnt[wave][w[q]] = base + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  uint32_t hc = 0, ih = 0;
+  uint32_t hc = 0, ih = 0, hv[WAVES];
   if (t < kWoBins) {
 #pragma unroll
-    for (uint32_t v = 0; v < WAVES; ++v) hc += L.cnt[v][t];
-    counts_col[(uint64_t)t * stride] = hc;
-    ih = hc;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)ih, d);
-      if (lane >= d) ih += u;
+    for (uint32_t v = 0; v < WAVES; ++v) {
+      hv[v] = L.cnt[v][t];
+      hc += hv[v];
     }
+    counts_col[(uint64_t)t * stride] = hc;
+    ih = wo_wave_incl_scan(hc);
     if (lane == 63) L.tsum[wave] = ih;
   }
   __syncthreads();
@@ -99,9 +115,8 @@ __device__ __forceinline__ void wo_rank_chunk(const uint32_t (&w)[STEPS], uint32
     for (uint32_t v = 0; v < wave; ++v) run += L.tsum[v];
 #pragma unroll
     for (uint32_t v = 0; v < WAVES; ++v) {
-      const uint32_t h = L.cnt[v][t];
       L.cnt[v][t] = run;
-      run += h;
+      run += hv[v];
     }
   }
   __syncthreads();
