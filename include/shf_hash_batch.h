@@ -339,8 +339,9 @@ SHF_HB_API int shf_win_order(const shf_hash128 *hashes, uint64_t n, uint32_t *pe
  * d_out, and their window order in d_perm / d_win_start exactly as
  * shf_win_order_async would compute it from d_out -- without reading d_out
  * back: the hashing kernel writes each key's window byte beside its record
- * into the workspace (for 16-B keys it also counts each 4096-key chunk's
- * windows), and the order passes work from those bytes. d_workspace: at least
+ * into the workspace (for 16-B keys it instead ranks each 4096-key chunk by
+ * window itself and writes the chunk's counts and order), and the order passes
+ * work from those. d_workspace: at least
  * shf_win_order_workspace_bytes(n) bytes, 16-B aligned. n < 2^32. Enqueued on
  * hip_stream like the other _async calls; variable-length key errors are
  * reported by shf_hash_batch_status() (an invalid key's record is not written
