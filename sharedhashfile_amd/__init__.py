@@ -158,6 +158,15 @@ def _check(rc, where):
 # ---------------------------------------------------------------------------
 # torch device-resident helpers (pointers are HBM addresses)
 # ---------------------------------------------------------------------------
+def _record(tensors, stream):
+    """Tensors allocated here on the current stream and used by kernels on `stream`:
+    the kernels may still run after the call returns, so keep the caching allocator
+    from handing their bytes out before `stream` gets there."""
+    if stream is not None:
+        for t in tensors:
+            t.record_stream(stream)
+
+
 def _stream_handle(stream):
     import torch
 
@@ -236,14 +245,17 @@ def hash_fixed(keys, key_len=None, seed=SEED, out=None, stream=None, kernel=KERN
         n, key_len = keys.shape
     else:
         n = keys.numel() // key_len if key_len else 0
+    mine = []
     if out is None:
         out = torch.empty((n, 2), dtype=torch.int64, device=keys.device)
+        mine.append(out)
     _require_out(out, (n, 2), (torch.int64,), keys.device)
     with _on(keys):
         rc = load().shf_hash_batch_fixed_kernel_async(
             ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()), kernel,
             _stream_handle(stream))
     _check(rc, "shf_hash_batch_fixed_kernel_async")
+    _record(mine, stream)
     return out
 
 
@@ -258,20 +270,24 @@ def hash_var(data, offsets, seed=SEED, out=None, stream=None, kernel=KERNEL_AUTO
 
     _require_cuda_u8(data, "data")
     n = _require_offsets(offsets, data)
+    mine = []
     if out is None:
         out = torch.empty((n, 2), dtype=torch.int64, device=data.device)
+        mine.append(out)
     _require_out(out, (n, 2), (torch.int64,), data.device)
     with _on(data):
         if key_bytes is None:
             rc = load().shf_hash_batch_var_kernel_async(
                 ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
                 ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
-            _check(rc, "shf_hash_batch_var_kernel_async")
-            return out
-        rc = load().shf_hash_batch_var_sized_kernel_async(
-            ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, int(key_bytes), seed,
-            ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
-    _check(rc, "shf_hash_batch_var_sized_kernel_async")
+            name = "shf_hash_batch_var_kernel_async"
+        else:
+            rc = load().shf_hash_batch_var_sized_kernel_async(
+                ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, int(key_bytes), seed,
+                ctypes.c_void_p(out.data_ptr()), kernel, _stream_handle(stream))
+            name = "shf_hash_batch_var_sized_kernel_async"
+    _check(rc, name)
+    _record(mine, stream)
     return out
 
 
@@ -284,14 +300,17 @@ def uid_parts_fixed(keys, key_len=None, seed=SEED, out=None, stream=None):
         n, key_len = keys.shape
     else:
         n = keys.numel() // key_len if key_len else 0
+    mine = []
     if out is None:
         out = torch.empty((n,), dtype=torch.int64, device=keys.device)
+        mine.append(out)
     _require_out(out, (n,), (torch.int64,), keys.device)
     with _on(keys):
         rc = load().shf_uid_parts_batch_fixed_async(
             ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()),
             _stream_handle(stream))
     _check(rc, "shf_uid_parts_batch_fixed_async")
+    _record(mine, stream)
     return out
 
 
@@ -300,14 +319,17 @@ def uid_parts_var(data, offsets, seed=SEED, out=None, stream=None):
 
     _require_cuda_u8(data, "data")
     n = _require_offsets(offsets, data)
+    mine = []
     if out is None:
         out = torch.empty((n,), dtype=torch.int64, device=data.device)
+        mine.append(out)
     _require_out(out, (n,), (torch.int64,), data.device)
     with _on(data):
         rc = load().shf_uid_parts_batch_var_async(
             ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
             ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_uid_parts_batch_var_async")
+    _record(mine, stream)
     return out
 
 
@@ -410,16 +432,21 @@ def probe_fixed(index, keys, key_len=None, seed=SEED, out=None, hashes=False, st
         n, key_len = keys.shape
     else:
         n = keys.numel() // key_len if key_len else 0
+    mine = []
     if out is None:
         out = torch.empty((n, 4), dtype=torch.int32, device=keys.device)
+        mine.append(out)
     _require_out(out, (n, 4), (torch.int32,), keys.device)
     hout = torch.empty((n, 2), dtype=torch.int64, device=keys.device) if hashes else None
+    if hout is not None:
+        mine.append(hout)
     with _on(keys):
         rc = load().shf_probe_batch_fixed_kernel_async(
             index.handle, ctypes.c_void_p(keys.data_ptr()), key_len, n, seed,
             ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()), kernel,
             _stream_handle(stream))
     _check(rc, "shf_probe_batch_fixed_kernel_async")
+    _record(mine, stream)
     return (out, hout) if hashes else out
 
 
@@ -428,16 +455,21 @@ def probe_var(index, data, offsets, seed=SEED, out=None, hashes=False, stream=No
 
     _require_cuda_u8(data, "data")
     n = _require_offsets(offsets, data)
+    mine = []
     if out is None:
         out = torch.empty((n, 4), dtype=torch.int32, device=data.device)
+        mine.append(out)
     _require_out(out, (n, 4), (torch.int32,), data.device)
     hout = torch.empty((n, 2), dtype=torch.int64, device=data.device) if hashes else None
+    if hout is not None:
+        mine.append(hout)
     with _on(data):
         rc = load().shf_probe_batch_var_async(
             index.handle, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
             ctypes.c_void_p(hout.data_ptr() if hout is not None else 0), ctypes.c_void_p(out.data_ptr()),
             _stream_handle(stream))
     _check(rc, "shf_probe_batch_var_async")
+    _record(mine, stream)
     return (out, hout) if hashes else out
 
 
@@ -449,13 +481,16 @@ def probe_hashes(index, hashes, out=None, stream=None):
     if hashes.dim() != 2 or hashes.shape[1] != 2:
         raise ValueError("hashes must have shape (n, 2)")
     n = hashes.shape[0]
+    mine = []
     if out is None:
         out = torch.empty((n, 4), dtype=torch.int32, device=hashes.device)
+        mine.append(out)
     _require_out(out, (n, 4), (torch.int32,), hashes.device)
     with _on(hashes):
         rc = load().shf_probe_batch_hashes_async(index.handle, ctypes.c_void_p(hashes.data_ptr()), n,
                                                  ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
     _check(rc, "shf_probe_batch_hashes_async")
+    _record(mine, stream)
     return out
 
 
@@ -470,68 +505,72 @@ def win_order(hashes, perm=None, win_start=None, workspace=None, stream=None):
         raise ValueError("hashes must have shape (n, 2)")
     n = hashes.shape[0]
     dev = hashes.device
+    mine = []  # tensors allocated here (on the current stream)
     if perm is None:
         perm = torch.empty(n, dtype=torch.int32, device=dev)
+        mine.append(perm)
     _require_out(perm, (n,), (torch.int32,), dev)
     if win_start is None:
         win_start = torch.empty(257, dtype=torch.int32, device=dev)
+        mine.append(win_start)
     _require_out(win_start, (257,), (torch.int32,), dev)
     lib = load()
     need = lib.shf_win_order_workspace_bytes(n)
-    own_ws = workspace is None
-    if own_ws:
+    if workspace is None:
         workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        mine.append(workspace)
     _require_cuda_u8(workspace, "workspace")
     with _on(hashes):
         rc = lib.shf_win_order_async(ctypes.c_void_p(hashes.data_ptr()), n, ctypes.c_void_p(perm.data_ptr()),
                                      ctypes.c_void_p(win_start.data_ptr()), ctypes.c_void_p(workspace.data_ptr()),
                                      workspace.numel(), _stream_handle(stream))
     _check(rc, "shf_win_order_async")
-    if stream is not None and own_ws:
-        # the kernels still read the scratch on `stream` after this returns: keep the
-        # caching allocator from handing its bytes out before that stream gets there
-        workspace.record_stream(stream)
+    _record(mine, stream)
     return perm, win_start
 
 
 def _win_outputs(n, dev, out, perm, win_start, workspace):
     import torch
 
+    mine = []  # tensors allocated here (on the current stream)
     if out is None:
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        mine.append(out)
     _require_out(out, (n, 2), _offset_dtypes(), dev)
     if perm is None:
         perm = torch.empty(n, dtype=torch.int32, device=dev)
+        mine.append(perm)
     _require_out(perm, (n,), (torch.int32,), dev)
     if win_start is None:
         win_start = torch.empty(257, dtype=torch.int32, device=dev)
+        mine.append(win_start)
     _require_out(win_start, (257,), (torch.int32,), dev)
-    own_ws = workspace is None
-    if own_ws:
+    if workspace is None:
         workspace = torch.empty(max(load().shf_win_order_workspace_bytes(n), 1), dtype=torch.uint8, device=dev)
+        mine.append(workspace)
     _require_cuda_u8(workspace, "workspace")
-    return out, perm, win_start, workspace, own_ws
+    return out, perm, win_start, workspace, mine
 
 
 def hash_fixed_win(keys, key_len, seed=SEED, out=None, perm=None, win_start=None, workspace=None, stream=None,
                    kernel=KERNEL_AUTO):
     """Hash + window order in one call (shf_hash_batch_fixed_win_async):
     returns (hashes (n, 2) int64, perm int32[n], win_start int32[257]), the
-    order exactly what win_order(hashes) gives, computed from the window bytes
-    the hashing kernel writes beside the records."""
+    order exactly what win_order(hashes) gives, computed without reading the
+    records back (16-B keys: the hashing kernel ranks each chunk itself; other
+    lengths: it writes each key's window byte beside its record)."""
     _require_cuda_u8(keys, "keys")
     if key_len <= 0 or keys.numel() % key_len:
         raise ValueError("keys.numel() must be a multiple of key_len")
     n = keys.numel() // key_len
-    out, perm, win_start, workspace, own_ws = _win_outputs(n, keys.device, out, perm, win_start, workspace)
+    out, perm, win_start, workspace, mine = _win_outputs(n, keys.device, out, perm, win_start, workspace)
     with _on(keys):
         rc = load().shf_hash_batch_fixed_win_kernel_async(
             ctypes.c_void_p(keys.data_ptr()), key_len, n, seed, ctypes.c_void_p(out.data_ptr()),
             ctypes.c_void_p(perm.data_ptr()), ctypes.c_void_p(win_start.data_ptr()),
             ctypes.c_void_p(workspace.data_ptr()), workspace.numel(), kernel, _stream_handle(stream))
     _check(rc, "shf_hash_batch_fixed_win_kernel_async")
-    if stream is not None and own_ws:
-        workspace.record_stream(stream)
+    _record(mine, stream)
     return out, perm, win_start
 
 
@@ -543,15 +582,14 @@ def hash_var_win(data, offsets, seed=SEED, out=None, perm=None, win_start=None, 
     n = offsets.numel() - 1
     if n < 0:
         raise ValueError("offsets needs n + 1 entries")
-    out, perm, win_start, workspace, own_ws = _win_outputs(n, data.device, out, perm, win_start, workspace)
+    out, perm, win_start, workspace, mine = _win_outputs(n, data.device, out, perm, win_start, workspace)
     with _on(data):
         rc = load().shf_hash_batch_var_win_kernel_async(
             ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), n, seed,
             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(perm.data_ptr()), ctypes.c_void_p(win_start.data_ptr()),
             ctypes.c_void_p(workspace.data_ptr()), workspace.numel(), kernel, _stream_handle(stream))
     _check(rc, "shf_hash_batch_var_win_kernel_async")
-    if stream is not None and own_ws:
-        workspace.record_stream(stream)
+    _record(mine, stream)
     return out, perm, win_start
 
 

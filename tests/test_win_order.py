@@ -209,6 +209,34 @@ def test_win_order_on_a_side_stream_outside_its_context(hb, dev, oracle):
 
 
 @pytest.mark.gpu
+def test_fused_outputs_on_a_side_stream_outside_its_context(hb, dev, oracle):
+    """The same for the fused calls and the plain hash: every tensor the wrapper
+    allocates (records, perm, win_start, workspace) is reserved for the stream
+    the kernels run on, so allocator churn on the current stream meanwhile
+    cannot overwrite them before those kernels ran."""
+    import torch
+
+    rng = np.random.default_rng(37)
+    n = 200_000
+    kn = rng.integers(0, 256, size=n * 16, dtype=np.uint8)
+    keys = torch.from_numpy(kn).to(dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    want_h = oracle.hash_fixed(kn, 16)
+    want_p, want_s = oracle.win_order(want_h)
+    for _ in range(3):
+        h, perm, start = hb.hash_fixed_win(keys, 16, stream=s)
+        h2 = hb.hash_fixed(keys, 16, stream=s)
+        junk = [torch.full((1 << 20,), 7, dtype=torch.uint8, device=dev) for _ in range(16)]  # reuse freed blocks
+        del junk
+        s.synchronize()
+        np.testing.assert_array_equal(h.cpu().numpy().view(np.uint64), want_h)
+        np.testing.assert_array_equal(h2.cpu().numpy().view(np.uint64), want_h)
+        np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), want_p)
+        np.testing.assert_array_equal(start.cpu().numpy().view(np.uint32), want_s)
+
+
+@pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref/libref_shf.so not built")
 def test_gpu_window_order_drives_the_reference_put(hb, dev, oracle):
     """End to end: GPU hashes and GPU window order drive the reference's own
