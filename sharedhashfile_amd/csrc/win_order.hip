@@ -186,7 +186,8 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_place(const uint16_t* __restr
 #pragma unroll
   for (uint32_t q = 0; q < kPer; ++q) {
     const uint32_t j = t + kWoThreads * q;
-    if (j < kn) perm[gdelta[win_at[j]] + j] = (uint32_t)(k0 + e[q]);
+    const uint32_t at = gdelta[win_at[j]] + j;
+    if (j < kn && at < n) perm[at] = (uint32_t)(k0 + e[q]);  // at < n always, unless the counts were not this batch's
   }
 }
 
