@@ -71,7 +71,7 @@ extern "C" {
 
 /* Where the caller's buffers live. */
 #define SHF_HASH_MEM_DEVICE 0 /* keys, offsets and out are device (HBM) pointers */
-#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); staged through pinned buffers, or read and written by the kernel in place (page-locked fixed-length buffers) */
+#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); staged through pinned buffers, or read and written by the kernel in place (page-locked fixed-length buffers; pageable ones only with SHF_HB_PAGEABLE_ZERO_COPY=1) */
 
 /* One result record: identical bytes to SHF_HASH (shf.private.h:180-185). */
 typedef struct shf_hash128 {

@@ -662,14 +662,21 @@ struct PageLock {
 // the range only partly covers go through the staged pipeline. A partial page
 // is never locked, so calls over neighbouring parts of one buffer (the
 // *_multi shards) never lock, or unlock, a page the other one uses.
+// Opt-in (SHF_HB_PAGEABLE_ZERO_COPY=1) since round 4: in 2 of 2 full GPU test
+// runs with it on by default, a later pageable hipMemcpy of the test process
+// (torch's .to(device) of a numpy array) failed with an illegal address, and
+// with it off 204 of 204 tests passed: registering and
+// unregistering ranges of the caller's pageable memory appears to leave the
+// runtime's own pageable-copy path a stale mapping. The product must not make a
+// caller's unrelated copies fault, so the default is the staged pipeline.
 // Returns 1 when it does not apply (then nothing was launched).
 constexpr uint64_t kPage = 4096;
 constexpr uint64_t kPageableZeroCopyMin = (uint64_t)1 << 16;  // keys: below this, locking pages costs more
 
 int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                   const HostJob& job) {
-  const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");
-  if ((e && e[0] == '0') || n < kPageableZeroCopyMin) return 1;
+  const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");  // opt-in: "1"
+  if (!(e && e[0] == '1') || n < kPageableZeroCopyMin) return 1;
   const uint64_t kb = reinterpret_cast<uintptr_t>(keys), ob = reinterpret_cast<uintptr_t>(job.hash);
   const uint64_t kp0 = (kb + kPage - 1) & ~(kPage - 1), kp1 = (kb + n * key_len) & ~(kPage - 1);
   const uint64_t op0 = (ob + kPage - 1) & ~(kPage - 1), op1 = (ob + n * sizeof(shf_hash128)) & ~(kPage - 1);
