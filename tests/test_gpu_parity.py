@@ -503,33 +503,6 @@ def test_host_zero_copy(hb, dev, oracle, monkeypatch, key_len):
     assert np.array_equal(one.numpy().view(np.uint64), want[:1])
 
 
-@pytest.mark.parametrize("key_len,kpad,opad", [(16, 0, 0), (16, 48, 16), (24, 7, 32), (100, 4093, 4080)])
-def test_host_pageable_zero_copy(hb, dev, oracle, monkeypatch, key_len, kpad, opad):
-    """Pageable caller buffers: the pages wholly inside the key and hash
-    ranges are page-locked for the call and read / written by the kernel over
-    PCIe, the keys at the ends go through the staged pipeline. Interior
-    offsets put the range ends mid-page (and unaligned keys on k_generic); the
-    same bits as the oracle with the path on, off, and with nothing beside
-    the caller's range touched."""
-    lib = hb.load()
-    n = 300_007
-    kbuf = np.frombuffer(splitmix_bytes(n * key_len + kpad + 64, 41 + key_len), dtype=np.uint8).copy()
-    flat = kbuf[kpad:kpad + n * key_len]
-    want = oracle.hash_fixed(flat, key_len, threads=8)
-    for env in ("1", "0"):
-        monkeypatch.setenv("SHF_HB_PAGEABLE_ZERO_COPY", env)
-        obuf = np.zeros(n * 16 + opad + 64, dtype=np.uint8)
-        rc = lib.shf_hash_batch_fixed(kbuf.ctypes.data + kpad, key_len, n, 12345, obuf.ctypes.data + opad,
-                                      hb.MEM_HOST)
-        assert rc == 0, env
-        got = obuf[opad:opad + n * 16].view(np.uint64).reshape(n, 2)
-        assert np.array_equal(got, want), env
-        assert not obuf[:opad].any() and not obuf[opad + n * 16:].any(), env
-    # the buffers are pageable again afterwards (each call unlocked what it locked)
-    assert lib.shf_hash_batch_fixed(kbuf.ctypes.data + kpad, key_len, n, 12345, obuf.ctypes.data + opad,
-                                    hb.MEM_HOST) == 0
-
-
 def test_multi_shards_share_boundary_pages(hb, dev, oracle, monkeypatch):
     """*_multi shards over one pageable buffer, split mid-page: each shard
     locks only the pages wholly inside its own key and hash ranges, so the
