@@ -87,20 +87,25 @@ constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `con
 // Shape of the host-memory pipelines: SHF_HB_STAGE_MB MiB of key bytes per
 // chunk, SHF_HB_SLOTS (2..4) chunks in flight, one stream each. Both are read on
 // every call (tools/host_pipeline_sweep.py, profiles/r1/host_pipeline_sweep.txt).
+// Defaults per key kind (the environment sets both): variable-length keys
+// 32 MiB x 3 (U[8,512] B from pageable buffers 0.193 G keys/s, 8 MiB x 4:
+// 0.181); fixed-length keys 8 MiB x 4 (10M x 16 B: pageable 2.04, page-locked
+// staged 2.19 G keys/s; 32 MiB x 3: 1.50, 1.89; 4 and 2 MiB slower again:
+// profiles/r4/stage_sweep/).
 constexpr int kMaxSlots = 4;
-constexpr long kDefaultStageMb = 32;  // 10M x 16 B: pageable 1.49, pinned 1.86 G keys/s (64 MiB x 2: 1.36, 1.75)
-constexpr int kDefaultSlots = 3;
+constexpr long kDefaultStageMb = 32, kDefaultStageMbFixed = 8;
+constexpr int kDefaultSlots = 3, kDefaultSlotsFixed = 4;
 
-size_t stage_bytes() {
+size_t stage_bytes(bool fixed = false) {
   const char* e = getenv("SHF_HB_STAGE_MB");
   const long mb = e ? strtol(e, nullptr, 10) : 0;
-  return (size_t)(mb >= 1 && mb <= 4096 ? mb : kDefaultStageMb) << 20;
+  return (size_t)(mb >= 1 && mb <= 4096 ? mb : fixed ? kDefaultStageMbFixed : kDefaultStageMb) << 20;
 }
 
-int pipeline_slots() {
+int pipeline_slots(bool fixed = false) {
   const char* e = getenv("SHF_HB_SLOTS");
   const long v = e ? strtol(e, nullptr, 10) : 0;
-  return v >= 2 && v <= kMaxSlots ? (int)v : kDefaultSlots;
+  return v >= 2 && v <= kMaxSlots ? (int)v : fixed ? kDefaultSlotsFixed : kDefaultSlots;
 }
 
 shfhb::Sink out_sink(void* out) {
@@ -734,9 +739,9 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
       if (rc != 1) return rc;
     }
   }
-  if ((uint64_t)key_len > stage_bytes()) return host_fixed_big(c, keys, key_len, n, seed, job);
-  const int ns = pipeline_slots();
-  const uint64_t per = key_len ? std::max<uint64_t>(1, stage_bytes() / key_len) : (uint64_t)1 << 22;
+  if ((uint64_t)key_len > stage_bytes(true)) return host_fixed_big(c, keys, key_len, n, seed, job);
+  const int ns = pipeline_slots(true);
+  const uint64_t per = key_len ? std::max<uint64_t>(1, stage_bytes(true) / key_len) : (uint64_t)1 << 22;
   const uint64_t chunk = std::min<uint64_t>(per, n);
   if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk, ns))) return rc;
   if (job.probe && (rc = ensure_probe_staging(c))) return rc;
