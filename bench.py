@@ -328,7 +328,7 @@ def grid_threads(name, n):
     if name == "tabpart":
         return n * 512                  # k_tab_split: one 512-thread workgroup per tab
     if name in ("winorder", "hashwin16"):
-        return (n + 4095) // 4096 * 256  # k_wo_place (and k_wo_rank): one 256-thread workgroup per 4096 keys
+        return (n + 4095) // 4096 * 256  # k_wo_rank: one 256-thread workgroup per 4096 keys
     return None
 
 

@@ -138,14 +138,18 @@ __global__ __launch_bounds__(256) void k_wo_scan_rows(uint32_t* __restrict__ cou
 // in perm and its first position in the chunk's order; gdelta = their
 // difference + the chunk's prefix (k_wo_scan_rows). Thread b marks positions
 // [first, first + count) as window b's; then position j of the order goes to
-// perm[gdelta[window of j] + j] (thread t the positions t, t + 256, ...: a
+// perm[gdelta[window of j] + j] (thread t the positions t, t + 512, ...: a
 // window's keys are consecutive both in the order and in perm, so each store
 // instruction writes a few runs of whole lines). The order's entries are loaded
-// first, their latency under the scans.
-__global__ __launch_bounds__(kWoThreads) void k_wo_place(const uint16_t* __restrict__ sorted, uint64_t n,
-                                                        const uint32_t* __restrict__ counts,
-                                                        uint32_t* __restrict__ perm, uint32_t* __restrict__ win_start) {
-  constexpr uint32_t kPer = kWoChunk / kWoThreads;
+// first, their latency under the scans. 512 threads (threads b < 256 do the
+// per-window work): 16.6 us per 10M keys against 17.3 with 256.
+constexpr uint32_t kWoPlaceThreads = 512;
+
+__global__ __launch_bounds__(kWoPlaceThreads) void k_wo_place(const uint16_t* __restrict__ sorted, uint64_t n,
+                                                             const uint32_t* __restrict__ counts,
+                                                             uint32_t* __restrict__ perm,
+                                                             uint32_t* __restrict__ win_start) {
+  constexpr uint32_t kPer = kWoChunk / kWoPlaceThreads;
   __shared__ uint32_t gdelta[kWoBins];  // window t's perm position minus its position in the chunk's order
   __shared__ __attribute__((aligned(16))) uint8_t win_at[kWoChunk];  // the window of each position of the order
   __shared__ uint32_t tsum[2][4];
@@ -155,27 +159,32 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_place(const uint16_t* __restr
   const uint32_t kn = (uint32_t)min<uint64_t>(kWoChunk, n - k0);
   uint32_t e[kPer];
 #pragma unroll
-  for (uint32_t q = 0; q < kPer; ++q) e[q] = sorted[k0 + t + kWoThreads * q];  // whole chunks in the workspace
-  const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
-  const uint32_t tot = row[gridDim.x], pre = row[c];
-  const uint32_t hc = row[c + 1] - pre;  // entry [chunks] is the total: the last chunk's difference holds too
-  const uint32_t it = wo_wave_incl_scan(tot), ih = wo_wave_incl_scan(hc);
-  if (lane == 63) {
-    tsum[0][wave] = it;
-    tsum[1][wave] = ih;
+  for (uint32_t q = 0; q < kPer; ++q) e[q] = sorted[k0 + t + kWoPlaceThreads * q];  // whole chunks in the workspace
+  uint32_t tot = 0, pre = 0, hc = 0, it = 0, ih = 0;
+  if (t < kWoBins) {
+    const uint32_t* row = counts + (uint64_t)t * wo_row_stride(gridDim.x);
+    tot = row[gridDim.x];
+    pre = row[c];
+    hc = row[c + 1] - pre;  // entry [chunks] is the total: the last chunk's difference holds too
+    it = wo_wave_incl_scan(tot);
+    ih = wo_wave_incl_scan(hc);
+    if (lane == 63) {
+      tsum[0][wave] = it;
+      tsum[1][wave] = ih;
+    }
   }
   __syncthreads();
-  uint32_t bbase = it - tot, lbase = ih - hc;
-  for (uint32_t v = 0; v < wave; ++v) {
-    bbase += tsum[0][v];
-    lbase += tsum[1][v];
-  }
-  if (c == 0 && win_start) {
-    win_start[t] = bbase;
-    if (t == kWoThreads - 1) win_start[kWoBins] = bbase + tot;  // = n
-  }
-  gdelta[t] = bbase + pre - lbase;
-  {
+  if (t < kWoBins) {
+    uint32_t bbase = it - tot, lbase = ih - hc;
+    for (uint32_t v = 0; v < wave; ++v) {
+      bbase += tsum[0][v];
+      lbase += tsum[1][v];
+    }
+    if (c == 0 && win_start) {
+      win_start[t] = bbase;
+      if (t == kWoBins - 1) win_start[kWoBins] = bbase + tot;  // = n
+    }
+    gdelta[t] = bbase + pre - lbase;
     uint32_t j = lbase;
     const uint32_t je = lbase + hc;
     for (; j < je && (j & 3u); ++j) win_at[j] = (uint8_t)t;
@@ -185,7 +194,7 @@ __global__ __launch_bounds__(kWoThreads) void k_wo_place(const uint16_t* __restr
   __syncthreads();
 #pragma unroll
   for (uint32_t q = 0; q < kPer; ++q) {
-    const uint32_t j = t + kWoThreads * q;
+    const uint32_t j = t + kWoPlaceThreads * q;
     const uint32_t at = gdelta[win_at[j]] + j;
     if (j < kn && at < n) perm[at] = (uint32_t)(k0 + e[q]);  // at < n always, unless the counts were not this batch's
   }
@@ -229,7 +238,7 @@ hipError_t launch_win_order_bytes(uint64_t n, bool ranked, uint32_t* perm, uint3
     hipLaunchKernelGGL(k_wo_rank_bytes, dim3(chunks), dim3(kWoThreads), 0, st, win_order_wins(workspace, n), n,
                        counts, sorted);
   hipLaunchKernelGGL(k_wo_scan_rows, dim3(kWoBins), dim3(256), 0, st, counts, chunks);
-  hipLaunchKernelGGL(k_wo_place, dim3(chunks), dim3(kWoThreads), 0, st, sorted, n, counts, perm, win_start);
+  hipLaunchKernelGGL(k_wo_place, dim3(chunks), dim3(kWoPlaceThreads), 0, st, sorted, n, counts, perm, win_start);
   return hipGetLastError();
 }
 
