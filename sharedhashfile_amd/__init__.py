@@ -107,6 +107,7 @@ _SIGS = {
     "shf_hash_batch_device_count": [],
     "shf_hash_batch_check_device": [],
     "shf_hash_batch_last_hip_error": [],
+    "shf_hash_batch_release": [],
     "shf_hash_batch_strerror": [_INT],
     "shf_hash_batch_version": [],
 }

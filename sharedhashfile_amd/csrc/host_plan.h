@@ -1,0 +1,254 @@
+// Host-only arithmetic of the host-memory pipelines (shf_hash_batch.hip), kept
+// free of HIP so that it compiles with g++ -fsanitize=address,undefined and is
+// unit-tested on the CPU (tests/c/test_host_plan.cpp, tests/test_host_plan.py):
+//
+//   * slot_layout / fixed_chunk_keys / var_chunk_end: how one chunk of keys, its
+//     hash records, probe records and offsets are carved out of one staging slot
+//     (a pinned host arena and a device arena of the same size);
+//   * page_split: which whole pages of a pageable caller buffer the pageable
+//     zero copy may page-lock, and which keys they carry;
+//   * SlotPool: the per-device pool of staging slots that every calling thread
+//     borrows from (a bounded footprint per process, not per thread).
+//
+// Key lengths follow the reference's contract: MurmurHash3_x64_128 takes
+// `const int len` (/root/reference/src/murmurhash3.c:75), so a key is < 2^31 B;
+// variable-length batches are validated (offsets non-decreasing, lengths < 2^31)
+// before any of this runs (check_var_lengths_host).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <vector>
+
+namespace shfhb {
+namespace plan {
+
+constexpr size_t kAlign = 256;  // every region of a slot starts 256-B aligned (16-B kernel loads, whole lines)
+constexpr size_t kMinSlotBytes = (size_t)64 << 10;
+constexpr size_t kHashBytes = 16, kProbeBytes = 16, kOffBytes = 8;
+
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// Byte offsets of one chunk's buffers inside a slot arena: keys at 0, then the
+// hash records, the probe records (when asked) and the cnt + 1 offsets (when asked).
+struct SlotLayout {
+  size_t out = 0, probe = 0, off = 0, end = 0;
+};
+
+inline SlotLayout slot_layout(size_t in_bytes, uint64_t cnt, bool probe, bool offsets) {
+  SlotLayout l;
+  size_t o = align_up(in_bytes);
+  l.out = o;
+  o += align_up((size_t)cnt * kHashBytes);
+  l.probe = o;
+  if (probe) o += align_up((size_t)cnt * kProbeBytes);
+  l.off = o;
+  if (offsets) o += align_up(((size_t)cnt + 1) * kOffBytes);
+  l.end = o;
+  return l;
+}
+
+// Most fixed-length keys of key_len bytes one slot of slot_bytes holds with
+// their records; 0 when not even one does (the key then goes through a
+// temporary device buffer of its own).
+inline uint64_t fixed_chunk_keys(size_t slot_bytes, uint32_t key_len, bool probe) {
+  const size_t per = (size_t)key_len + kHashBytes + (probe ? kProbeBytes : 0);
+  auto fits = [&](uint64_t c) { return slot_layout((size_t)c * key_len, c, probe, false).end <= slot_bytes; };
+  if (!fits(1)) return 0;
+  // within a few keys of the answer (the regions' alignment costs at most 3 x kAlign bytes)
+  uint64_t c = slot_bytes > 3 * kAlign ? std::max<uint64_t>(1, (slot_bytes - 3 * kAlign) / per) : 1;
+  while (c > 1 && !fits(c)) --c;
+  while (fits(c + 1)) ++c;
+  return c;
+}
+
+// Variable-length keys from key i0 (offsets[i0..n] non-decreasing): the end i1 of
+// the longest chunk [i0, i1) whose key bytes, records and offsets fit one slot.
+// A single key too long for the slot gives i1 = i0 + 1 with *alone = true: its
+// bytes go through a temporary device buffer, its record and offsets through the slot.
+inline uint64_t var_chunk_end(const uint64_t* offsets, uint64_t i0, uint64_t n, size_t slot_bytes, bool probe,
+                              bool* alone) {
+  const uint64_t base = offsets[i0];
+  // each key costs at least its record and offset: no chunk holds more keys than this
+  const uint64_t cap = std::max<uint64_t>(1, slot_bytes / (kHashBytes + kOffBytes));
+  uint64_t lo = i0 + 1, hi = std::min(n, i0 + std::min(cap, n - i0));
+  auto fits = [&](uint64_t i1) { return slot_layout(offsets[i1] - base, i1 - i0, probe, true).end <= slot_bytes; };
+  *alone = !fits(lo);
+  if (*alone) return lo;
+  // largest i1 in [lo, hi] that fits (fits() is monotone: offsets never decrease)
+  while (lo < hi) {
+    const uint64_t mid = lo + (hi - lo + 1) / 2;
+    if (fits(mid))
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+// Pageable zero copy (shf_hash_batch.hip host_fixed_pageable_zero_copy): the
+// whole pages [kp0, kp1) inside the keys' bytes [kb, kb + n * key_len) and
+// [op0, op1) inside the records [ob, ob + 16 n), and the keys [lo, hi) whose
+// bytes and record lie wholly in those pages. ok = false when there is no such
+// range of at least min_keys keys, the two page ranges overlap, or the ranges
+// do not fit the address space.
+struct PageSplit {
+  bool ok = false;
+  uint64_t kp0 = 0, kp1 = 0, op0 = 0, op1 = 0, lo = 0, hi = 0;
+};
+
+inline PageSplit page_split(uint64_t kb, uint32_t key_len, uint64_t n, uint64_t ob, uint64_t page,
+                            uint64_t min_keys) {
+  PageSplit r;
+  uint64_t kbytes = 0, obytes = 0, kend = 0, oend = 0;
+  if (!key_len || !n || !page || (page & (page - 1))) return r;
+  if (__builtin_mul_overflow(n, (uint64_t)key_len, &kbytes) || __builtin_mul_overflow(n, (uint64_t)kHashBytes, &obytes) ||
+      __builtin_add_overflow(kb, kbytes, &kend) || __builtin_add_overflow(ob, obytes, &oend) || kb > UINT64_MAX - page ||
+      ob > UINT64_MAX - page)
+    return r;
+  r.kp0 = (kb + page - 1) & ~(page - 1);
+  r.kp1 = kend & ~(page - 1);
+  r.op0 = (ob + page - 1) & ~(page - 1);
+  r.op1 = oend & ~(page - 1);
+  if (r.kp1 <= r.kp0 || r.op1 <= r.op0) return r;
+  if (r.kp1 > r.op0 && r.op1 > r.kp0) return r;  // key and record pages overlap
+  r.lo = std::max((r.kp0 - kb + key_len - 1) / key_len, (r.op0 - ob + kHashBytes - 1) / kHashBytes);
+  r.hi = std::min((r.kp1 - kb) / key_len, (r.op1 - ob) / kHashBytes);
+  r.ok = r.hi > r.lo && r.hi - r.lo >= min_keys;
+  return r;
+}
+
+// A bounded pool of staging slots, shared by every thread of the process that
+// stages host memory for one device. A call borrows between one and `want`
+// slots: the first blocks until a slot is free (or may be made), the others are
+// taken only if free right now, so no caller ever waits while holding slots and
+// the pool cannot deadlock (as long as no caller borrows again while it holds
+// slots: the library never nests its leases). Slots are made lazily, at most max_slots of them at
+// once, and one of another size (SHF_HB_STAGE_MB changed) is remade on reuse.
+// Slot must have a `size_t bytes` member; make/unmake allocate and free one.
+template <class Slot>
+class SlotPool {
+ public:
+  using Make = std::function<int(size_t bytes, Slot** out)>;
+  using Unmake = std::function<void(Slot*)>;
+
+  SlotPool(Make make, Unmake unmake) : make_(std::move(make)), unmake_(std::move(unmake)) {}
+
+  // Borrows 1..want slots of `bytes` each into out[]; returns 0 and their number in *got,
+  // or the first error of `make` (then nothing is held). A slot counts against max_slots
+  // from the moment it is to be made until it has been freed, so the memory the pool
+  // holds never exceeds max_slots slots, even while sizes change.
+  int acquire(size_t bytes, int want, int max_slots, Slot** out, int* got) {
+    *got = 0;
+    max_slots = std::max(1, max_slots);
+    for (;;) {
+      std::vector<Slot*> stale;
+      int to_make = 0;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        max_slots_ = max_slots;
+        bytes_ = bytes;
+        auto can = [&] { return !idle_.empty() || live_ < max_slots_; };
+        cv_.wait(lk, can);
+        while (*got + to_make < want && can()) {
+          if (!idle_.empty()) {
+            Slot* s = idle_.back();
+            idle_.pop_back();
+            if (s->bytes != bytes)
+              stale.push_back(s);  // freed below, still counted until then
+            else
+              out[(*got)++] = s;
+          } else {
+            ++live_;
+            ++to_make;
+          }
+        }
+      }
+      forget(stale);
+      int rc = 0;
+      for (; to_make > 0; --to_make) {
+        Slot* s = nullptr;
+        const int r = rc ? rc : make_(bytes, &s);
+        if (r) {
+          rc = r;
+          std::lock_guard<std::mutex> lk(mu_);
+          --live_;
+          cv_.notify_all();
+          continue;
+        }
+        out[(*got)++] = s;
+      }
+      if (*got) return 0;  // with fewer slots than wanted if some could not be made
+      if (rc) return rc;
+      // only stale slots were found: they are freed now, try again
+    }
+  }
+
+  // Returns slots to the pool (their work must be finished); a slot of a stale
+  // size, or above the current cap, is freed instead.
+  void release(Slot** s, int n) {
+    std::vector<Slot*> drop;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      int live_after = live_;  // live_ itself drops once forget() has freed them
+      for (int i = 0; i < n; ++i) {
+        if (s[i]->bytes != bytes_ || live_after > max_slots_) {
+          drop.push_back(s[i]);
+          --live_after;
+        } else {
+          idle_.push_back(s[i]);
+        }
+      }
+    }
+    cv_.notify_all();
+    forget(drop);
+  }
+
+  // Frees every idle slot (slots on loan come back later and are kept).
+  void trim() {
+    std::vector<Slot*> drop;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      drop.swap(idle_);
+    }
+    forget(drop);
+  }
+
+  int live() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return live_;
+  }
+  int idle() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (int)idle_.size();
+  }
+
+ private:
+  Make make_;
+  Unmake unmake_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Slot*> idle_;
+  int live_ = 0;  // slots being made, idle, on loan or being freed
+  int max_slots_ = 1;
+  size_t bytes_ = 0;
+
+  // Frees slots taken out of the pool, then stops counting them.
+  void forget(std::vector<Slot*>& v) {
+    if (v.empty()) return;
+    for (Slot* x : v) unmake_(x);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      live_ -= (int)v.size();
+    }
+    cv_.notify_all();
+    v.clear();
+  }
+};
+
+}  // namespace plan
+}  // namespace shfhb

@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -27,6 +28,7 @@
 
 #include "../../include/shf_hash_batch.h"
 #include "kernels.h"
+#include "host_plan.h"
 
 // Row index: device copies of a store's tab map and rows (shf_hash_batch.h).
 struct shf_row_index {
@@ -84,28 +86,36 @@ bool debug_errors() {
   } while (0)
 
 constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `const int len`
-// Shape of the host-memory pipelines: SHF_HB_STAGE_MB MiB of key bytes per
-// chunk, SHF_HB_SLOTS (2..4) chunks in flight, one stream each. Both are read on
-// every call (tools/host_pipeline_sweep.py, profiles/r1/host_pipeline_sweep.txt).
-// Defaults per key kind (the environment sets both): variable-length keys
-// 32 MiB x 3 (U[8,512] B from pageable buffers 0.193 G keys/s, 8 MiB x 4:
-// 0.181); fixed-length keys 8 MiB x 4 (10M x 16 B: pageable 2.04, page-locked
-// staged 2.19 G keys/s; 32 MiB x 3: 1.50, 1.89; 4 and 2 MiB slower again:
-// profiles/r4/stage_sweep/).
+// Shape of the host-memory pipelines. Every process stages through one pool of
+// slots per device (host_plan.h SlotPool), shared by all calling threads: a
+// slot is a pinned host arena and a device arena of SHF_HB_STAGE_MB MiB each
+// (default 16) with its own stream, and the pool holds at most SHF_HB_POOL_MB
+// MiB of them (default 64, i.e. 64 MiB of device and 64 MiB of pinned memory
+// per device, whatever the number of threads). A call borrows up to
+// SHF_HB_SLOTS (1..4, default 4) slots, one chunk in flight on each. All three
+// are read on every call. A 16-MiB slot carries 512 Ki 16-B keys with their
+// records (the 8 MiB x 4 chunks of round 4: 10M x 16 B pageable 2.04, page-
+// locked staged 2.19 G keys/s; profiles/r4/stage_sweep/), or ~15 MiB of
+// variable-length keys with their offsets and records.
 constexpr int kMaxSlots = 4;
-constexpr long kDefaultStageMb = 32, kDefaultStageMbFixed = 8;
-constexpr int kDefaultSlots = 3, kDefaultSlotsFixed = 4;
+constexpr long kDefaultStageMb = 16, kDefaultPoolMb = 64;
 
-size_t stage_bytes(bool fixed = false) {
+size_t stage_bytes() {
   const char* e = getenv("SHF_HB_STAGE_MB");
   const long mb = e ? strtol(e, nullptr, 10) : 0;
-  return (size_t)(mb >= 1 && mb <= 4096 ? mb : fixed ? kDefaultStageMbFixed : kDefaultStageMb) << 20;
+  return (size_t)(mb >= 1 && mb <= 4096 ? mb : kDefaultStageMb) << 20;
 }
 
-int pipeline_slots(bool fixed = false) {
+size_t pool_bytes() {
+  const char* e = getenv("SHF_HB_POOL_MB");
+  const long mb = e ? strtol(e, nullptr, 10) : 0;
+  return (size_t)(mb >= 1 && mb <= (1L << 20) ? mb : kDefaultPoolMb) << 20;
+}
+
+int pipeline_slots() {
   const char* e = getenv("SHF_HB_SLOTS");
   const long v = e ? strtol(e, nullptr, 10) : 0;
-  return v >= 2 && v <= kMaxSlots ? (int)v : fixed ? kDefaultSlotsFixed : kDefaultSlots;
+  return v >= 1 && v <= kMaxSlots ? (int)v : kMaxSlots;
 }
 
 shfhb::Sink out_sink(void* out) {
@@ -114,24 +124,103 @@ shfhb::Sink out_sink(void* out) {
   return k;
 }
 
-// Per (thread, device) resources. Created lazily, reused across calls.
+// One staging slot of a device's pool: chunks are carved out of the arenas by
+// host_plan.h slot_layout (keys, hash records, probe records, offsets).
+struct Slot {
+  int dev = -1;
+  size_t bytes = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* h = nullptr;      // pinned host arena
+  uint8_t* h_dev = nullptr;  // its device address (kernels store records there over PCIe), or null
+  uint8_t* d = nullptr;      // device arena
+};
+
+void unmake_slot(Slot* s) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(s->dev);
+  if (s->st) (void)hipStreamSynchronize(s->st);
+  if (s->h) (void)hipHostFree(s->h);
+  if (s->d) (void)hipFree(s->d);
+  if (s->done) (void)hipEventDestroy(s->done);
+  if (s->st) (void)hipStreamDestroy(s->st);
+  (void)hipGetLastError();
+  (void)hipSetDevice(prev);
+  delete s;
+}
+
+int make_slot(int dev, size_t bytes, Slot** out) {
+  Slot* s = new Slot();
+  s->dev = dev;
+  s->bytes = bytes;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(dev);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&s->h, bytes, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc((void**)&s->d, bytes);
+  if (e == hipSuccess && hipHostGetDevicePointer((void**)&s->h_dev, s->h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    s->h_dev = nullptr;
+  }
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    const int rc = map_hip(e);
+    unmake_slot(s);
+    return rc;
+  }
+  *out = s;
+  return SHF_HB_OK;
+}
+
+using Pool = shfhb::plan::SlotPool<Slot>;
+
+// The process's pools, one per device, made on first use and kept for the
+// process's life (shf_hash_batch_release() frees their idle slots).
+std::mutex g_pools_mu;
+std::map<int, Pool*> g_pools;
+
+Pool* device_pool(int dev) {
+  std::lock_guard<std::mutex> g(g_pools_mu);
+  Pool*& p = g_pools[dev];
+  if (!p)
+    p = new Pool([dev](size_t bytes, Slot** out) { return make_slot(dev, bytes, out); },
+                 [](Slot* s) { unmake_slot(s); });
+  return p;
+}
+
+// The slots one call borrows; given back (after their streams are idle) when it ends.
+struct Lease {
+  Pool* pool = nullptr;
+  Slot* s[kMaxSlots] = {};
+  int n = 0;
+  Lease() = default;
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+  ~Lease() {
+    if (!n) return;
+    for (int i = 0; i < n; ++i) (void)hipStreamSynchronize(s[i]->st);  // on every path, errors included
+    (void)hipGetLastError();
+    pool->release(s, n);
+  }
+};
+
+int lease_slots(int dev, int want, Lease* L) {
+  const size_t bytes = std::max(stage_bytes(), shfhb::plan::kMinSlotBytes);
+  const int max_slots = (int)std::max<size_t>(1, std::min<size_t>(64, pool_bytes() / bytes));
+  L->pool = device_pool(dev);
+  return L->pool->acquire(bytes, std::min(std::max(want, 1), kMaxSlots), max_slots, L->s, &L->n);
+}
+
+// Per (thread, device) state, made lazily and kept across calls: one stream for
+// launches that stage nothing, the variable-length status words and the
+// window-order buffers. No staging: that is the process pool's.
 struct DevCtx {
   int dev = -1;
   int status = SHF_HB_OK;
-  hipStream_t st[kMaxSlots] = {};
-  hipEvent_t done[kMaxSlots] = {};
-  uint8_t* h_in[kMaxSlots] = {};
-  uint8_t* d_in[kMaxSlots] = {};
-  size_t in_cap = 0;
-  shf_hash128* h_out[kMaxSlots] = {};
-  shf_hash128* d_out[kMaxSlots] = {};
-  uint64_t* h_off[kMaxSlots] = {};
-  uint64_t* d_off[kMaxSlots] = {};
-  size_t key_cap = 0;  // records in h_out/d_out and offsets (+1) per slot
-  shf_probe* h_probe[kMaxSlots] = {};  // row pre-probe records (allocated on first use)
-  shf_probe* d_probe[kMaxSlots] = {};
-  size_t probe_cap = 0;
-  int n_staged = 0;  // slots whose staging buffers are allocated
+  hipStream_t st = nullptr;
   // Variable-length key checks done by the kernels (kernels.h Sink::status):
   // word 0 collects this thread's async calls until shf_hash_batch_status()
   // takes it (word 2 receives the taken value), word 1 is cleared and read by
@@ -146,10 +235,10 @@ struct DevCtx {
 
 void release_ctx(DevCtx* c);
 
-// The calling thread's contexts, one per device, freed when the thread exits
-// (streams, events, pinned and device staging). Not on the main thread at
-// process exit: the HIP runtime may already be going away, and the process's
-// memory goes with it anyway.
+// The calling thread's contexts, one per device, freed when the thread exits.
+// Not on the main thread at process exit (the HIP runtime may already be going
+// away, and the process's memory goes with it anyway): the main thread calls
+// shf_hash_batch_release() for that.
 struct ThreadCtxs {
   std::map<int, DevCtx*> m;
   ~ThreadCtxs() {
@@ -182,52 +271,22 @@ int current_ctx(DevCtx** out) {
   DevCtx* c = new DevCtx();
   c->dev = dev;
   c->status = check_arch(dev);
-  if (c->status == SHF_HB_OK) {
-    for (int s = 0; s < kMaxSlots && c->status == SHF_HB_OK; ++s) {
-      c->status = map_hip(hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking));
-      if (c->status == SHF_HB_OK) c->status = map_hip(hipEventCreateWithFlags(&c->done[s], hipEventDisableTiming));
-    }
-    if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 3 * sizeof(uint32_t)));
-    if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
-    if (c->status == SHF_HB_OK)
-      c->status = map_hip(hipHostMalloc((void**)&c->h_status, sizeof(uint32_t), hipHostMallocDefault));
-  }
+  if (c->status == SHF_HB_OK) c->status = map_hip(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+  if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 3 * sizeof(uint32_t)));
+  if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
+  if (c->status == SHF_HB_OK)
+    c->status = map_hip(hipHostMalloc((void**)&c->h_status, sizeof(uint32_t), hipHostMallocDefault));
   tls_ctx.m[dev] = c;
   *out = c;
   return c->status;
-}
-
-void free_staging(DevCtx* c) {
-  for (int s = 0; s < kMaxSlots; ++s) {
-    if (c->h_in[s]) (void)hipHostFree(c->h_in[s]);
-    if (c->d_in[s]) (void)hipFree(c->d_in[s]);
-    if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
-    if (c->d_out[s]) (void)hipFree(c->d_out[s]);
-    if (c->h_off[s]) (void)hipHostFree(c->h_off[s]);
-    if (c->d_off[s]) (void)hipFree(c->d_off[s]);
-    if (c->h_probe[s]) (void)hipHostFree(c->h_probe[s]);
-    if (c->d_probe[s]) (void)hipFree(c->d_probe[s]);
-    c->h_in[s] = c->d_in[s] = nullptr;
-    c->h_out[s] = c->d_out[s] = nullptr;
-    c->h_off[s] = c->d_off[s] = nullptr;
-    c->h_probe[s] = c->d_probe[s] = nullptr;
-  }
-  c->in_cap = c->key_cap = c->probe_cap = 0;
-  c->n_staged = 0;
 }
 
 void release_ctx(DevCtx* c) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(c->dev);
-  for (int s = 0; s < kMaxSlots; ++s) {
-    if (c->st[s]) (void)hipStreamSynchronize(c->st[s]);
-  }
-  free_staging(c);
-  for (int s = 0; s < kMaxSlots; ++s) {
-    if (c->done[s]) (void)hipEventDestroy(c->done[s]);
-    if (c->st[s]) (void)hipStreamDestroy(c->st[s]);
-  }
+  if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->st) (void)hipStreamDestroy(c->st);
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);
   if (c->d_win_ws) (void)hipFree(c->d_win_ws);
@@ -237,41 +296,21 @@ void release_ctx(DevCtx* c) {
   delete c;
 }
 
-// Release every context of this thread now (the *_multi workers, before they
-// report back; other threads are covered by ThreadCtxs at thread exit).
+// Release every context of this thread now (the *_multi workers before they
+// report back, and shf_hash_batch_release(); other threads are covered by
+// ThreadCtxs at thread exit).
 void release_thread_ctx() {
   for (auto& kv : tls_ctx.m) release_ctx(kv.second);
   tls_ctx.m.clear();
 }
 
-int ensure_staging(DevCtx* c, size_t in_bytes, size_t keys, int slots) {
-  if (in_bytes <= c->in_cap && keys <= c->key_cap && slots <= c->n_staged) return SHF_HB_OK;
-  for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
-  const size_t ib = std::max(in_bytes, c->in_cap), kc = std::max(keys, c->key_cap);
-  const int ns = std::max(slots, c->n_staged);
-  free_staging(c);
-  for (int s = 0; s < ns; ++s) {
-    HB_TRY(hipHostMalloc((void**)&c->h_in[s], ib, hipHostMallocDefault));
-    HB_TRY(hipMalloc((void**)&c->d_in[s], ib));
-    HB_TRY(hipHostMalloc((void**)&c->h_out[s], kc * sizeof(shf_hash128), hipHostMallocDefault));
-    HB_TRY(hipMalloc((void**)&c->d_out[s], kc * sizeof(shf_hash128)));
-    HB_TRY(hipHostMalloc((void**)&c->h_off[s], (kc + 1) * sizeof(uint64_t), hipHostMallocDefault));
-    HB_TRY(hipMalloc((void**)&c->d_off[s], (kc + 1) * sizeof(uint64_t)));
-  }
-  c->in_cap = ib;
-  c->key_cap = kc;
-  c->n_staged = ns;
-  return SHF_HB_OK;
-}
-
 // shf_win_order's workspace: grown when a batch needs more, else reused (a hipFree per call
-// would synchronise the device every batch). Every stream of the context is idle first.
+// would synchronise the device every batch). The context's stream and the null stream are idle first.
 int ensure_win_ws(DevCtx* c, size_t bytes, void** out) {
   if (bytes > c->win_ws_cap) {
-    for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
+    HB_TRY(hipStreamSynchronize(c->st));
     HB_TRY(hipStreamSynchronize(nullptr));
     if (c->d_win_ws) (void)hipFree(c->d_win_ws);
-  if (c->d_perm) (void)hipFree(c->d_perm);
     c->d_win_ws = nullptr;
     c->win_ws_cap = 0;
     HB_TRY(hipMalloc(&c->d_win_ws, bytes));
@@ -281,11 +320,12 @@ int ensure_win_ws(DevCtx* c, size_t bytes, void** out) {
   return SHF_HB_OK;
 }
 
-// Device room for a host-memory window order: n indices then 257 window starts (grows only).
+// Device room for a host-memory window order: n indices then 257 window starts (grows only;
+// this is the only function that frees or replaces d_perm).
 int ensure_perm(DevCtx* c, uint64_t n, uint32_t** out) {
   const size_t need = ((size_t)n + 257u) * sizeof(uint32_t);
   if (need > c->perm_cap) {
-    for (int s = 0; s < kMaxSlots; ++s) HB_TRY(hipStreamSynchronize(c->st[s]));
+    HB_TRY(hipStreamSynchronize(c->st));
     if (c->d_perm) (void)hipFree(c->d_perm);
     c->d_perm = nullptr;
     c->perm_cap = 0;
@@ -293,24 +333,6 @@ int ensure_perm(DevCtx* c, uint64_t n, uint32_t** out) {
     c->perm_cap = need;
   }
   *out = c->d_perm;
-  return SHF_HB_OK;
-}
-
-// Probe-record staging, key_cap records per slot (after ensure_staging).
-int ensure_probe_staging(DevCtx* c) {
-  if (c->probe_cap >= c->key_cap) return SHF_HB_OK;
-  for (int s = 0; s < kMaxSlots; ++s) {
-    HB_TRY(hipStreamSynchronize(c->st[s]));
-    if (c->h_probe[s]) (void)hipHostFree(c->h_probe[s]);
-    if (c->d_probe[s]) (void)hipFree(c->d_probe[s]);
-    c->h_probe[s] = c->d_probe[s] = nullptr;
-  }
-  c->probe_cap = 0;
-  for (int s = 0; s < c->n_staged; ++s) {
-    HB_TRY(hipHostMalloc((void**)&c->h_probe[s], c->key_cap * sizeof(shf_probe), hipHostMallocDefault));
-    HB_TRY(hipMalloc((void**)&c->d_probe[s], c->key_cap * sizeof(shf_probe)));
-  }
-  c->probe_cap = c->key_cap;
   return SHF_HB_OK;
 }
 
@@ -436,11 +458,13 @@ struct HostJob {
   uint8_t* wins = nullptr;  // device: the batch's window bytes (kOutHashWin), key i's at wins[i]
 };
 
-// One chunk in flight per slot; `pending` remembers where its results go.
+// One chunk in flight per slot; where its results go once the slot's event fires.
 struct Pending {
   bool busy = false;
-  shf_hash128* hash = nullptr;  // nullptr: not requested, or DMA'd straight to the caller
+  shf_hash128* hash = nullptr;  // nullptr: not requested, or DMA'd / stored straight to the caller
+  const shf_hash128* hash_src = nullptr;  // the slot's pinned records to copy from
   shf_probe* probe = nullptr;
+  const shf_probe* probe_src = nullptr;
   uint64_t count = 0;
 };
 
@@ -458,6 +482,7 @@ bool trace_on() {
 struct PipeTrace {
   double copy_in = 0, wait = 0, copy_out = 0, enqueue = 0;
   uint64_t chunks = 0;
+  int slots = 0;
 };
 thread_local PipeTrace tls_trace;
 
@@ -465,14 +490,14 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int drain_slot(DevCtx* c, int s, Pending& p) {
+int drain_slot(Slot* s, Pending& p) {
   if (!p.busy) return SHF_HB_OK;
   const bool tr = trace_on();
   const double t0 = tr ? now_ms() : 0;
-  HB_TRY(hipEventSynchronize(c->done[s]));
+  HB_TRY(hipEventSynchronize(s->done));
   const double t1 = tr ? now_ms() : 0;
-  if (p.hash) par_memcpy(p.hash, c->h_out[s], p.count * sizeof(shf_hash128));
-  if (p.probe) par_memcpy(p.probe, c->h_probe[s], p.count * sizeof(shf_probe));
+  if (p.hash) par_memcpy(p.hash, p.hash_src, p.count * sizeof(shf_hash128));
+  if (p.probe) par_memcpy(p.probe, p.probe_src, p.count * sizeof(shf_probe));
   if (tr) {
     tls_trace.wait += t1 - t0;
     tls_trace.copy_out += now_ms() - t1;
@@ -481,14 +506,42 @@ int drain_slot(DevCtx* c, int s, Pending& p) {
   return SHF_HB_OK;
 }
 
-void* host_range_device_ptr(const void* p, size_t bytes);
+int drain_all(Lease& L, Pending* pend) {
+  for (int q = 0; q < L.n; ++q) {
+    const int rc = drain_slot(L.s[q], pend[q]);
+    if (rc) return rc;
+  }
+  return SHF_HB_OK;
+}
 
-// Kernel output of slot s for `job`, chunk [i0, ...).
-void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k, int* mode) {
+// One chunk's buffers inside a slot (host_plan.h slot_layout).
+struct ChunkBufs {
+  uint8_t *h_in, *d_in;
+  shf_hash128 *h_out, *d_out, *hd_out;  // hd_out: device address of h_out, or null
+  shf_probe *h_probe, *d_probe;
+  uint64_t *h_off, *d_off;
+};
+
+ChunkBufs carve(const Slot* s, const shfhb::plan::SlotLayout& l) {
+  ChunkBufs b;
+  b.h_in = s->h;
+  b.d_in = s->d;
+  b.h_out = reinterpret_cast<shf_hash128*>(s->h + l.out);
+  b.d_out = reinterpret_cast<shf_hash128*>(s->d + l.out);
+  b.hd_out = s->h_dev ? reinterpret_cast<shf_hash128*>(s->h_dev + l.out) : nullptr;
+  b.h_probe = reinterpret_cast<shf_probe*>(s->h + l.probe);
+  b.d_probe = reinterpret_cast<shf_probe*>(s->d + l.probe);
+  b.h_off = reinterpret_cast<uint64_t*>(s->h + l.off);
+  b.d_off = reinterpret_cast<uint64_t*>(s->d + l.off);
+  return b;
+}
+
+// Kernel output of one chunk [i0, ...) for `job`.
+void job_sink(const ChunkBufs& b, const HostJob& job, uint64_t i0, shfhb::Sink* k, int* mode) {
   *k = shfhb::Sink();
   if (job.probe) {
-    k->out = c->d_probe[s];
-    k->hash_out = job.hash ? c->d_out[s] : nullptr;
+    k->out = b.d_probe;
+    k->hash_out = job.hash ? b.d_out : nullptr;
     k->tab_slot = job.index->d_tab_slot;
     if (job.index->compact && !job.index->external) {
       k->map8 = job.index->d_map8;
@@ -498,8 +551,7 @@ void job_sink(DevCtx* c, int s, const HostJob& job, uint64_t i0, shfhb::Sink* k,
     k->n_slots = job.index->n_slots;
     *mode = shfhb::kOutProbe;
   } else {
-    void* staged = job.stage_direct ? host_range_device_ptr(c->h_out[s], sizeof(shf_hash128)) : nullptr;
-    k->out = job.hash_dev ? job.hash_dev + i0 : staged ? staged : c->d_out[s];
+    k->out = job.hash_dev ? job.hash_dev + i0 : (job.stage_direct && b.hd_out) ? b.hd_out : b.d_out;
     *mode = shfhb::kOutHash;
     if (job.wins) {
       k->wins = job.wins + i0;
@@ -517,55 +569,69 @@ int direct_sink(const HostJob& job, void* d_out, shfhb::Sink* k) {
 }
 
 // Results of chunk [i0, i0 + cnt) back to the caller (straight into page-locked
-// caller memory, else into the slot's staging for drain_slot to copy).
-int job_d2h(DevCtx* c, int s, const HostJob& job, uint64_t i0, uint64_t cnt, bool hash_pinned, bool probe_pinned,
-            Pending* p) {
-  *p = Pending{true, nullptr, nullptr, cnt};
-  if (job.hash && !job.hash_dev && job.stage_direct && !job.probe &&
-      host_range_device_ptr(c->h_out[s], sizeof(shf_hash128))) {
-    p->hash = job.hash + i0;  // the kernel stored into h_out[s] (job_sink): drain_slot copies out
+// caller memory, else into the slot's pinned arena for drain_slot to copy).
+int job_d2h(Slot* s, const ChunkBufs& b, const HostJob& job, uint64_t i0, uint64_t cnt, bool hash_pinned,
+            bool probe_pinned, Pending* p) {
+  *p = Pending();
+  p->busy = true;
+  p->count = cnt;
+  if (job.hash && !job.hash_dev && job.stage_direct && !job.probe && b.hd_out) {
+    p->hash = job.hash + i0;  // the kernel stored into the slot's pinned records (job_sink): copied out by drain_slot
+    p->hash_src = b.h_out;
   } else if (job.hash && !job.hash_dev) {
-    HB_TRY(hipMemcpyAsync(hash_pinned ? job.hash + i0 : c->h_out[s], c->d_out[s], cnt * sizeof(shf_hash128),
-                          hipMemcpyDeviceToHost, c->st[s]));
-    if (!hash_pinned) p->hash = job.hash + i0;
+    HB_TRY(hipMemcpyAsync(hash_pinned ? job.hash + i0 : b.h_out, b.d_out, cnt * sizeof(shf_hash128),
+                          hipMemcpyDeviceToHost, s->st));
+    if (!hash_pinned) {
+      p->hash = job.hash + i0;
+      p->hash_src = b.h_out;
+    }
   }
   if (job.probe) {
-    HB_TRY(hipMemcpyAsync(probe_pinned ? job.probe + i0 : c->h_probe[s], c->d_probe[s], cnt * sizeof(shf_probe),
-                          hipMemcpyDeviceToHost, c->st[s]));
-    if (!probe_pinned) p->probe = job.probe + i0;
+    HB_TRY(hipMemcpyAsync(probe_pinned ? job.probe + i0 : b.h_probe, b.d_probe, cnt * sizeof(shf_probe),
+                          hipMemcpyDeviceToHost, s->st));
+    if (!probe_pinned) {
+      p->probe = job.probe + i0;
+      p->probe_src = b.h_probe;
+    }
   }
-  HB_TRY(hipEventRecord(c->done[s], c->st[s]));
+  HB_TRY(hipEventRecord(s->done, s->st));
   return SHF_HB_OK;
 }
 
-// A device buffer for keys larger than the staging (SHF_HB_STAGE_MB): allocated
-// for the one chunk that needs it and freed with it, so the per-slot staging
-// never grows past the stage size.
+// A device buffer for one key larger than a slot: allocated for the chunk that
+// needs it and freed with it (after the stream that reads it is idle), so the
+// slots never grow past the stage size.
 struct TmpDevBuf {
   void* p = nullptr;
+  hipStream_t st = nullptr;
   ~TmpDevBuf() {
-    if (p) (void)hipFree(p);
+    if (!p) return;
+    if (st) (void)hipStreamSynchronize(st);
+    (void)hipFree(p);
   }
 };
 
-// Fixed-length keys larger than the stage: one key at a time on slot 0,
-// through a temporary device buffer (pageable sources are staged by HIP).
-int host_fixed_big(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
-  int rc = ensure_staging(c, 1, 1, pipeline_slots());
+// Fixed-length keys larger than a slot: one key at a time on one slot, through
+// a temporary device buffer (pageable sources are staged by HIP).
+int host_fixed_big(int dev, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job) {
+  Lease L;
+  int rc = lease_slots(dev, 1, &L);
   if (rc) return rc;
-  if (job.probe && (rc = ensure_probe_staging(c))) return rc;
+  Slot* s = L.s[0];
+  const ChunkBufs b = carve(s, shfhb::plan::slot_layout(0, 1, job.probe != nullptr, false));
   TmpDevBuf tmp;
+  tmp.st = s->st;
   HB_TRY(hipMalloc(&tmp.p, key_len));
   const bool hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
   for (uint64_t i = 0; i < n; ++i) {
     Pending p;
-    HB_TRY(hipMemcpyAsync(tmp.p, keys + i * (uint64_t)key_len, key_len, hipMemcpyHostToDevice, c->st[0]));
+    HB_TRY(hipMemcpyAsync(tmp.p, keys + i * (uint64_t)key_len, key_len, hipMemcpyHostToDevice, s->st));
     shfhb::Sink k;
     int mode = 0;
-    job_sink(c, 0, job, i, &k, &mode);
-    HB_TRY(shfhb::launch_fixed(tmp.p, key_len, 1, seed, k, mode, c->st[0], shfhb::kKernelAuto));
-    if ((rc = job_d2h(c, 0, job, i, 1, hash_pinned, probe_pinned, &p))) return rc;
-    if ((rc = drain_slot(c, 0, p))) return rc;
+    job_sink(b, job, i, &k, &mode);
+    HB_TRY(shfhb::launch_fixed(tmp.p, key_len, 1, seed, k, mode, s->st, shfhb::kKernelAuto));
+    if ((rc = job_d2h(s, b, job, i, 1, hash_pinned, probe_pinned, &p))) return rc;
+    if ((rc = drain_slot(s, p))) return rc;
   }
   return SHF_HB_OK;
 }
@@ -622,13 +688,42 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
                    bool direct = true);
 HostJob hash_job(shf_hash128* out);
 
+// SHF_HB_TRACE_LOCKS=1 (read once): every page lock and unlock of the pageable
+// zero copy is printed on stderr with its range and the runtime's answers.
+bool trace_locks() {
+  static const bool on = [] {
+    const char* e = getenv("SHF_HB_TRACE_LOCKS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// Does the runtime hold a registration covering host address p? (hipHostRegister'd or
+// hipHostMalloc'd: the runtime then resolves p to a device mapping for every copy and kernel.)
+bool runtime_registered(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Registrations of caller pages this library failed to end (hipHostUnregister failed, or the
+// runtime still resolved the range afterwards). A registration that outlives the caller's
+// buffer gives the next buffer mapped at that address a stale device mapping: any pageable
+// copy from it then fails with hipErrorIllegalAddress (tools/pageable_register_repro.hip,
+// scenario D). Never expected to be non-zero; the pageable zero copy refuses to run once it is.
+std::atomic<int> g_lock_leaks{0};
+
 // Page-locks [p, p + bytes) (whole pages) for one call and unlocks it after.
 struct PageLock {
   void* p = nullptr;
   void* dev = nullptr;
+  size_t bytes = 0;
   std::pair<uintptr_t, uintptr_t> range{0, 0};  // listed in g_lib_locks while non-empty
-  bool lock(void* at, size_t bytes) {
-    const std::pair<uintptr_t, uintptr_t> r{reinterpret_cast<uintptr_t>(at), reinterpret_cast<uintptr_t>(at) + bytes};
+  bool lock(void* at, size_t n) {
+    const std::pair<uintptr_t, uintptr_t> r{reinterpret_cast<uintptr_t>(at), reinterpret_cast<uintptr_t>(at) + n};
     {
       // pages another call of this library holds: leave them to it (concurrent hipHostRegister
       // of one range, and unlocking under the other call's kernel, are both avoided)
@@ -638,25 +733,48 @@ struct PageLock {
       g_lib_locks.push_back(r);
     }
     range = r;
-    if (hipHostRegister(at, bytes, hipHostRegisterMapped) != hipSuccess) {
+    // pages the runtime already resolves (the caller's own registration): not ours to lock
+    if (runtime_registered(at) || runtime_registered(static_cast<uint8_t*>(at) + n - 1)) return false;
+    const hipError_t e = hipHostRegister(at, n, hipHostRegisterMapped);
+    if (trace_locks()) fprintf(stderr, "shf_hash_batch lock [%p, +%zu) -> %d\n", at, n, (int)e);
+    if (e != hipSuccess) {
       (void)hipGetLastError();  // e.g. pages another call (or the caller) has locked: not ours to use
       return false;
     }
     p = at;
+    bytes = n;
     if (hipHostGetDevicePointer(&dev, at, 0) != hipSuccess) {
       (void)hipGetLastError();
       return false;
     }
     return true;
   }
-  ~PageLock() {
-    if (p && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+  // Ends the registration; SHF_HB_ERR_HIP if the runtime still resolves the range after it.
+  int unlock() {
+    int rc = SHF_HB_OK;
+    if (p) {
+      const hipError_t e = hipHostUnregister(p);
+      if (e != hipSuccess) (void)hipGetLastError();
+      const bool still = runtime_registered(p) || runtime_registered(static_cast<uint8_t*>(p) + bytes - 1);
+      if (trace_locks())
+        fprintf(stderr, "shf_hash_batch unlock [%p, +%zu) -> %d%s\n", p, bytes, (int)e, still ? " STILL REGISTERED" : "");
+      if (e != hipSuccess || still) {
+        g_lock_leaks.fetch_add(1);
+        if (debug_errors()) fprintf(stderr, "shf_hash_batch: page lock [%p, +%zu) not ended (%d)\n", p, bytes, (int)e);
+        tls_last_hip = e != hipSuccess ? (int)e : (int)hipErrorHostMemoryAlreadyRegistered;
+        rc = SHF_HB_ERR_HIP;
+      }
+      p = nullptr;
+    }
     if (range.second) {  // after the unlock (equal entries of other calls are interchangeable)
       std::lock_guard<std::mutex> g(g_lib_lock_mu);
       const auto it = std::find(g_lib_locks.begin(), g_lib_locks.end(), range);
       if (it != g_lib_locks.end()) g_lib_locks.erase(it);
+      range = {0, 0};
     }
+    return rc;
   }
+  ~PageLock() { (void)unlock(); }
 };
 
 // Pageable caller buffers, zero copy. The pages that lie wholly inside the
@@ -681,26 +799,25 @@ constexpr uint64_t kPageableZeroCopyMin = (uint64_t)1 << 16;  // keys: below thi
 int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                   const HostJob& job) {
   const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");  // opt-in: "1"
-  if (!(e && e[0] == '1') || n < kPageableZeroCopyMin) return 1;
+  if (!(e && e[0] == '1') || n < kPageableZeroCopyMin || g_lock_leaks.load()) return 1;
+  // keys [lo, hi): every byte in [kp0, kp1) and every record in [op0, op1) (host_plan.h)
+  const shfhb::plan::PageSplit ps = shfhb::plan::page_split(reinterpret_cast<uintptr_t>(keys), key_len, n,
+                                                            reinterpret_cast<uintptr_t>(job.hash), kPage,
+                                                            kPageableZeroCopyMin);
+  if (!ps.ok) return 1;
   const uint64_t kb = reinterpret_cast<uintptr_t>(keys), ob = reinterpret_cast<uintptr_t>(job.hash);
-  const uint64_t kp0 = (kb + kPage - 1) & ~(kPage - 1), kp1 = (kb + n * key_len) & ~(kPage - 1);
-  const uint64_t op0 = (ob + kPage - 1) & ~(kPage - 1), op1 = (ob + n * sizeof(shf_hash128)) & ~(kPage - 1);
-  if (kp1 <= kp0 || op1 <= op0) return 1;
-  // keys [lo, hi): every byte in [kp0, kp1) and every record in [op0, op1)
-  const uint64_t lo = std::max((kp0 - kb + key_len - 1) / key_len, (op0 - ob + 15) / 16);
-  const uint64_t hi = std::min((kp1 - kb) / key_len, (op1 - ob) / 16);
-  if (hi <= lo || hi - lo < kPageableZeroCopyMin) return 1;
-  if (kp1 > op0 && op1 > kp0) return 1;  // key and hash pages overlap: leave it to the pipeline
+  const uint64_t lo = ps.lo, hi = ps.hi;
   PageLock lk, lo_;
-  if (!lk.lock(reinterpret_cast<void*>(kp0), kp1 - kp0) || !lo_.lock(reinterpret_cast<void*>(op0), op1 - op0))
+  if (!lk.lock(reinterpret_cast<void*>(ps.kp0), ps.kp1 - ps.kp0) ||
+      !lo_.lock(reinterpret_cast<void*>(ps.op0), ps.op1 - ps.op0))
     return 1;  // e.g. already page-locked by someone else: the staged pipeline instead
-  const uint8_t* dk = static_cast<const uint8_t*>(lk.dev) + (kb + lo * key_len - kp0);
-  shf_hash128* dh = reinterpret_cast<shf_hash128*>(static_cast<uint8_t*>(lo_.dev) + (ob + lo * 16 - op0));
+  const uint8_t* dk = static_cast<const uint8_t*>(lk.dev) + (kb + lo * key_len - ps.kp0);
+  shf_hash128* dh = reinterpret_cast<shf_hash128*>(static_cast<uint8_t*>(lo_.dev) + (ob + lo * 16 - ps.op0));
   shfhb::Sink mk;
   int mmode = direct_sink(job, dh, &mk);
   if (mk.wins) mk.wins += lo;
-  HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, mk, mmode, c->st[0], shfhb::kKernelAuto));
-  // the ends meanwhile, through the staged pipeline (its slots queue behind the launch on st[0]),
+  HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, mk, mmode, c->st, shfhb::kKernelAuto));
+  // the ends meanwhile, through the staged pipeline (on the pool's slots, beside the launch),
   // copied through the staging as pageable memory: they may begin inside the pages just locked and
   // run past them, so they must not be taken for page-locked buffers
   int rc = SHF_HB_OK;
@@ -709,10 +826,11 @@ int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_l
   tail.wins = job.wins ? job.wins + hi : nullptr;
   if (lo) rc = host_fixed_run(keys, key_len, lo, seed, head, false);
   if (rc == SHF_HB_OK && hi < n) rc = host_fixed_run(keys + hi * key_len, key_len, n - hi, seed, tail, false);
-  const hipError_t se = hipStreamSynchronize(c->st[0]);  // before the pages are unlocked
+  const hipError_t se = hipStreamSynchronize(c->st);  // before the pages are unlocked
+  const int ru = lk.unlock(), rv = lo_.unlock();
   if (rc) return rc;
   HB_TRY(se);
-  return SHF_HB_OK;
+  return ru ? ru : rv;
 }
 
 // Host-memory fixed-length pipeline on the current device. direct = false: the
@@ -730,8 +848,8 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     if (dh) {
       shfhb::Sink dsk;
       const int dmode = direct_sink(job, dh, &dsk);
-      HB_TRY(shfhb::launch_fixed(dk, key_len, n, seed, dsk, dmode, c->st[0], shfhb::kKernelAuto));
-      HB_TRY(hipStreamSynchronize(c->st[0]));
+      HB_TRY(shfhb::launch_fixed(dk, key_len, n, seed, dsk, dmode, c->st, shfhb::kKernelAuto));
+      HB_TRY(hipStreamSynchronize(c->st));
       return SHF_HB_OK;
     }
     if (!is_host_pinned(keys) && !is_host_pinned(job.hash)) {
@@ -739,125 +857,106 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
       if (rc != 1) return rc;
     }
   }
-  if ((uint64_t)key_len > stage_bytes(true)) return host_fixed_big(c, keys, key_len, n, seed, job);
-  const int ns = pipeline_slots(true);
-  const uint64_t per = key_len ? std::max<uint64_t>(1, stage_bytes(true) / key_len) : (uint64_t)1 << 22;
-  const uint64_t chunk = std::min<uint64_t>(per, n);
-  if ((rc = ensure_staging(c, (size_t)chunk * key_len, (size_t)chunk, ns))) return rc;
-  if (job.probe && (rc = ensure_probe_staging(c))) return rc;
+  const bool probe = job.probe != nullptr;
+  if (!shfhb::plan::fixed_chunk_keys(std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), key_len, probe))
+    return host_fixed_big(c->dev, keys, key_len, n, seed, job);
+  Lease L;
+  if ((rc = lease_slots(c->dev, pipeline_slots(), &L))) return rc;
+  const uint64_t chunk = std::min<uint64_t>(shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe), n);
+  const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false);
   const bool in_pinned = direct && is_host_pinned(keys), hash_pinned = direct && is_host_pinned(job.hash),
              probe_pinned = direct && is_host_pinned(job.probe);
+  if (trace_on()) tls_trace.slots = L.n;
   Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += chunk, ++idx) {
-    const int s = (int)(idx % ns);
-    if ((rc = drain_slot(c, s, pend[s]))) return rc;
+    const int q = (int)(idx % L.n);
+    Slot* s = L.s[q];
+    if ((rc = drain_slot(s, pend[q]))) return rc;
+    const ChunkBufs b = carve(s, lay);
     const uint64_t cnt = std::min(chunk, n - i0);
     const size_t nb = (size_t)cnt * key_len;
-    const uint8_t* src = in_pinned ? keys + i0 * key_len : c->h_in[s];
+    const uint8_t* src = in_pinned ? keys + i0 * key_len : b.h_in;
     const double t0 = trace_on() ? now_ms() : 0;
-    if (nb && !in_pinned) par_memcpy(c->h_in[s], keys + i0 * key_len, nb);
+    if (nb && !in_pinned) par_memcpy(b.h_in, keys + i0 * key_len, nb);
     const double t1 = trace_on() ? now_ms() : 0;
-    if (nb) HB_TRY(hipMemcpyAsync(c->d_in[s], src, nb, hipMemcpyHostToDevice, c->st[s]));
+    if (nb) HB_TRY(hipMemcpyAsync(b.d_in, src, nb, hipMemcpyHostToDevice, s->st));
     shfhb::Sink k;
     int mode = 0;
-    job_sink(c, s, job, i0, &k, &mode);
-    HB_TRY(shfhb::launch_fixed(c->d_in[s], key_len, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto));
-    if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
+    job_sink(b, job, i0, &k, &mode);
+    HB_TRY(shfhb::launch_fixed(b.d_in, key_len, cnt, seed, k, mode, s->st, shfhb::kKernelAuto));
+    if ((rc = job_d2h(s, b, job, i0, cnt, hash_pinned, probe_pinned, &pend[q]))) return rc;
     if (trace_on()) {
       tls_trace.copy_in += t1 - t0;
       tls_trace.enqueue += now_ms() - t1;
       ++tls_trace.chunks;
     }
   }
-  for (int s = 0; s < ns; ++s)
-    if ((rc = drain_slot(c, s, pend[s]))) return rc;
-  return SHF_HB_OK;
+  return drain_all(L, pend);
 }
 
-// Host-memory variable-length pipeline: chunks of whole keys up to stage_bytes()
-// of key bytes (a single larger key gets a chunk of its own).
+// Host-memory variable-length pipeline: chunks of whole keys that fit one slot
+// with their offsets and records (host_plan.h var_chunk_end); a single key too
+// long for a slot gets a chunk of its own, its bytes in a temporary buffer.
 int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, const HostJob& job_in) {
   const HostJob job = with_direct_out(job_in, n);
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  const int ns = pipeline_slots();
-  const uint64_t stage = stage_bytes();
-  const uint64_t max_keys = std::min<uint64_t>(n, std::max<uint64_t>(stage / 16, (uint64_t)1 << 16));
+  const bool probe = job.probe != nullptr;
+  Lease L;
+  if ((rc = lease_slots(c->dev, pipeline_slots(), &L))) return rc;
+  const size_t slot_bytes = L.s[0]->bytes;
   const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
              hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
   Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
-    // extend the chunk while it fits the byte budget and key budget
-    uint64_t i1 = i0 + 1;
-    const uint64_t base = offsets[i0];
-    {
-      uint64_t lo = i1, hi = std::min(n, i0 + max_keys);
-      // largest i1 in [i0+1, hi] with offsets[i1] - base <= stage (offsets monotone)
-      while (lo < hi) {
-        const uint64_t mid = lo + (hi - lo + 1) / 2;
-        if (offsets[mid] - base <= stage) lo = mid;
-        else hi = mid - 1;
-      }
-      i1 = lo;
-    }
-    const uint64_t cnt = i1 - i0;
+    bool alone = false;
+    const uint64_t i1 = shfhb::plan::var_chunk_end(offsets, i0, n, slot_bytes, probe, &alone);
+    const uint64_t cnt = i1 - i0, base = offsets[i0];
     const size_t nb = (size_t)(offsets[i1] - base);
-    const bool big = nb > stage;  // one key larger than the stage: a temporary buffer, not bigger slots
-    const size_t in_need = big ? 1 : std::max(nb, (size_t)1);
-    const size_t need_keys = (size_t)std::max<uint64_t>(cnt, max_keys);
-    if (in_need > c->in_cap || need_keys > c->key_cap || c->n_staged < ns) {
-      // growing the staging buffers frees them: collect every chunk in flight first
-      for (int s = 0; s < ns; ++s)
-        if ((rc = drain_slot(c, s, pend[s]))) return rc;
-      if ((rc = ensure_staging(c, in_need, need_keys, ns))) return rc;
-    }
-    if (job.probe && (rc = ensure_probe_staging(c))) return rc;
-    const int s = (int)(idx % ns);
+    const int q = (int)(idx % L.n);
+    Slot* s = L.s[q];
     TmpDevBuf tmp;
-    if (big) {
-      for (int q = 0; q < ns; ++q)
-        if ((rc = drain_slot(c, q, pend[q]))) return rc;
+    if (alone) {
+      if ((rc = drain_all(L, pend))) return rc;
+      tmp.st = s->st;
       HB_TRY(hipMalloc(&tmp.p, nb));
-    } else if ((rc = drain_slot(c, s, pend[s]))) {
+    } else if ((rc = drain_slot(s, pend[q]))) {
       return rc;
     }
-    uint8_t* d_in = big ? (uint8_t*)tmp.p : c->d_in[s];
-    if (nb && !in_pinned && !big) par_memcpy(c->h_in[s], bytes + base, nb);
+    const ChunkBufs b = carve(s, shfhb::plan::slot_layout(alone ? 0 : nb, cnt, probe, true));
+    uint8_t* d_in = alone ? (uint8_t*)tmp.p : b.d_in;
+    if (nb && !in_pinned && !alone) par_memcpy(b.h_in, bytes + base, nb);
     const uint64_t* off_src = offsets + i0;
     if (!off_pinned) {
-      par_memcpy(c->h_off[s], offsets + i0, (cnt + 1) * sizeof(uint64_t));
-      off_src = c->h_off[s];
+      par_memcpy(b.h_off, offsets + i0, (cnt + 1) * sizeof(uint64_t));
+      off_src = b.h_off;
     }
     if (nb)
-      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || big) ? bytes + base : c->h_in[s], nb, hipMemcpyHostToDevice,
-                            c->st[s]));
-    HB_TRY(hipMemcpyAsync(c->d_off[s], off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->st[s]));
+      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || alone) ? bytes + base : b.h_in, nb, hipMemcpyHostToDevice, s->st));
+    HB_TRY(hipMemcpyAsync(b.d_off, off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s->st));
     shfhb::Sink k;
     int mode = 0;
-    job_sink(c, s, job, i0, &k, &mode);
+    job_sink(b, job, i0, &k, &mode);
     // the chunk's byte count sizes the span kernel's window (kernels.hip span_window)
-    HB_TRY(shfhb::launch_var(d_in, c->d_off[s], base, cnt, seed, k, mode, c->st[s], shfhb::kKernelAuto, nb));
-    if ((rc = job_d2h(c, s, job, i0, cnt, hash_pinned, probe_pinned, &pend[s]))) return rc;
-    if (big && (rc = drain_slot(c, s, pend[s]))) return rc;  // before tmp is freed
+    HB_TRY(shfhb::launch_var(d_in, b.d_off, base, cnt, seed, k, mode, s->st, shfhb::kKernelAuto, nb));
+    if ((rc = job_d2h(s, b, job, i0, cnt, hash_pinned, probe_pinned, &pend[q]))) return rc;
+    if (alone && (rc = drain_slot(s, pend[q]))) return rc;  // before tmp is freed
     i0 = i1;
   }
-  for (int s = 0; s < ns; ++s)
-    if ((rc = drain_slot(c, s, pend[s]))) return rc;
-  return SHF_HB_OK;
+  return drain_all(L, pend);
 }
 
-// On an error mid-pipeline, chunks may still be in flight, some DMA-ing into
-// the caller's (page-locked) output: wait for them before handing the buffers
-// back to the caller.
+// On an error mid-pipeline, work may still be in flight, some DMA-ing into the
+// caller's (page-locked) output: wait for it before handing the buffers back to
+// the caller (the slots' streams are waited for by their Lease).
 int drain_on_error(int rc) {
   if (rc == SHF_HB_OK) return rc;
   const int hip = tls_last_hip;
   DevCtx* c = nullptr;
-  if (current_ctx(&c) == SHF_HB_OK)
-    for (int s = 0; s < kMaxSlots; ++s) (void)hipStreamSynchronize(c->st[s]);
+  if (current_ctx(&c) == SHF_HB_OK) (void)hipStreamSynchronize(c->st);
   (void)hipGetLastError();
   tls_last_hip = hip;
   return rc;
@@ -898,7 +997,7 @@ int device_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, 
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  if (sync) st = c->st[0];
+  if (sync) st = nullptr;  // after the caller's null-stream work (e.g. the keys' producer)
   HB_TRY(shfhb::launch_fixed(keys, key_len, n, seed, sink, out_mode, st, kernel));
   if (sync) HB_TRY(hipStreamSynchronize(st));
   return SHF_HB_OK;
@@ -916,7 +1015,7 @@ int device_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t 
   if (rc) return rc;
   shfhb::Sink k = sink;
   if (sync) {
-    st = c->st[0];
+    st = nullptr;  // after the caller's null-stream work
     k.status = c->d_status + 1;
     HB_TRY(hipMemsetAsync(k.status, 0, sizeof(uint32_t), st));
   } else {
@@ -1201,7 +1300,9 @@ int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t 
   if (var && mem == SHF_HASH_MEM_HOST && (rc = check_var_lengths_host(offsets, n))) return rc;
   void* ws = nullptr;
   if ((rc = ensure_win_ws(c, (size_t)shfhb::win_order_workspace_bytes(n), &ws))) return rc;
-  const hipStream_t st = c->st[0];
+  // device memory: on the null stream, as every synchronous device entry point, so the
+  // hash and order run after whatever the caller enqueued there (e.g. the keys' producer)
+  const hipStream_t st = mem == SHF_HASH_MEM_DEVICE ? nullptr : c->st;
   if (mem == SHF_HASH_MEM_DEVICE) {
     shfhb::Sink k = out_sink(out);
     bool ranked = false;
@@ -1441,7 +1542,7 @@ int shf_tab_copy_batch(const void* src, uint64_t src_bytes, void* dst, uint64_t 
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  hipStream_t st = c->st[0];
+  hipStream_t st = mem == SHF_HASH_MEM_DEVICE ? nullptr : c->st;  // device memory: after the caller's null-stream work
   const size_t job_bytes = (size_t)n_jobs * sizeof(shf_tab_job), map_bytes = (size_t)n_maps * 2048u * 2u;
   if (mem == SHF_HASH_MEM_DEVICE) {
     HB_TRY(shfhb::launch_tab_split(src, src_bytes, dst, dst_bytes, jobs, n_jobs, maps, maps ? n_maps : 0, *params, st));
@@ -1495,7 +1596,7 @@ int shf_win_order(const shf_hash128* hashes, uint64_t n, uint32_t* perm, uint32_
   if (rc) return rc;
   // device memory: on the null stream, as the synchronous hashing calls do, so the order
   // runs after whatever the caller enqueued there (e.g. the hashes it orders)
-  hipStream_t st = mem == SHF_HASH_MEM_DEVICE ? nullptr : c->st[0];
+  hipStream_t st = mem == SHF_HASH_MEM_DEVICE ? nullptr : c->st;
   const size_t ws = (size_t)shfhb::win_order_workspace_bytes(n), ws_start = 257u * sizeof(uint32_t);
   void* d_ws = nullptr;
   if ((rc = ensure_win_ws(c, ws, &d_ws))) return rc;
@@ -1536,9 +1637,9 @@ int shf_hash_batch_status(void* hip_stream) {
   HB_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
   // read and clear in one atomic exchange on the device: a kernel on another
   // stream that flags a key meanwhile leaves the word set for the next query
-  HB_TRY(shfhb::launch_status_take(c->d_status, c->d_status + 2, c->st[0]));
-  HB_TRY(hipMemcpyAsync(c->h_status, c->d_status + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, c->st[0]));
-  HB_TRY(hipStreamSynchronize(c->st[0]));
+  HB_TRY(shfhb::launch_status_take(c->d_status, c->d_status + 2, c->st));
+  HB_TRY(hipMemcpyAsync(c->h_status, c->d_status + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+  HB_TRY(hipStreamSynchronize(c->st));
   return *c->h_status ? SHF_HB_ERR_ARG : SHF_HB_OK;
 }
 
@@ -1550,6 +1651,17 @@ int shf_hash_batch_check_device(void) {
 }
 
 int shf_hash_batch_last_hip_error(void) { return tls_last_hip; }
+
+int shf_hash_batch_release(void) {
+  release_thread_ctx();
+  std::vector<Pool*> pools;
+  {
+    std::lock_guard<std::mutex> g(g_pools_mu);
+    for (auto& kv : g_pools) pools.push_back(kv.second);
+  }
+  for (Pool* p : pools) p->trim();
+  return SHF_HB_OK;
+}
 
 const char* shf_hash_batch_strerror(int status) {
   switch (status) {

@@ -1,0 +1,247 @@
+// TEST INFRASTRUCTURE: unit tests of the host-only arithmetic of the host-memory
+// pipelines (sharedhashfile_amd/csrc/host_plan.h), built with
+// g++ -fsanitize=address,undefined by tests/c/Makefile (target `sanitize`) and
+// run by tests/test_host_plan.py on the CPU. Exit status 0 = every check held;
+// any sanitizer report aborts the program (-fno-sanitize-recover=all).
+//
+// Edge cases follow VERDICT r4 item 5: a buffer shorter than a page, key and
+// hash pages that overlap, key lengths and batches at the 2^31-byte limit of
+// the reference's `const int len` (/root/reference/src/murmurhash3.c:75).
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "../../sharedhashfile_amd/csrc/host_plan.h"
+
+using namespace shfhb::plan;
+
+static int failures = 0;
+#define CHECK(c)                                                     \
+  do {                                                               \
+    if (!(c)) {                                                      \
+      fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #c); \
+      ++failures;                                                    \
+    }                                                                \
+  } while (0)
+
+// Regions of a layout are aligned, disjoint, in order and inside the slot.
+static void check_layout(size_t slot, size_t in_bytes, uint64_t cnt, bool probe, bool offsets) {
+  const SlotLayout l = slot_layout(in_bytes, cnt, probe, offsets);
+  CHECK(l.out % kAlign == 0 && l.probe % kAlign == 0 && l.off % kAlign == 0 && l.end % kAlign == 0);
+  CHECK(l.out >= in_bytes);
+  CHECK(l.probe >= l.out + cnt * kHashBytes);
+  if (probe) CHECK(l.off >= l.probe + cnt * kProbeBytes);
+  if (offsets) CHECK(l.end >= l.off + (cnt + 1) * kOffBytes);
+  CHECK(l.end <= slot);
+}
+
+static void test_fixed_chunks() {
+  const size_t slots[] = {kMinSlotBytes, (size_t)1 << 20, (size_t)16 << 20, ((size_t)16 << 20) + 4096 + 17};
+  const uint32_t lens[] = {0, 1, 7, 15, 16, 17, 255, 256, 511, 4096, 65535, 1u << 20, (1u << 24) - 1};
+  for (size_t slot : slots)
+    for (uint32_t L : lens)
+      for (int probe = 0; probe < 2; ++probe) {
+        const uint64_t c = fixed_chunk_keys(slot, L, probe);
+        if (c) {
+          check_layout(slot, (size_t)c * L, c, probe, false);
+          // maximal: one more key does not fit
+          CHECK(slot_layout((size_t)(c + 1) * L, c + 1, probe, false).end > slot);
+        } else {
+          CHECK(slot_layout(L, 1, probe, false).end > slot);  // not even one key: the big-key path
+        }
+      }
+  // the default slot holds the round-4 chunk of 16-B keys (8 MiB of keys)
+  CHECK(fixed_chunk_keys((size_t)16 << 20, 16, false) == ((size_t)16 << 20) / 32);
+  // a key at the reference's limit never fits a slot
+  CHECK(fixed_chunk_keys((size_t)16 << 20, 0x7fffffffu, false) == 0);
+  CHECK(fixed_chunk_keys(2 * kAlign - 1, 1, false) == 0);  // not even the key's own 256-B region and its record
+}
+
+// Walks a batch the way host_var_run does and checks every chunk.
+static void walk_var(const std::vector<uint64_t>& off, size_t slot, bool probe) {
+  const uint64_t n = off.size() - 1;
+  uint64_t i0 = 0, chunks = 0;
+  while (i0 < n) {
+    bool alone = false;
+    const uint64_t i1 = var_chunk_end(off.data(), i0, n, slot, probe, &alone);
+    CHECK(i1 > i0 && i1 <= n);
+    if (i1 <= i0 || i1 > n) return;
+    const uint64_t nb = off[i1] - off[i0];
+    if (alone) {
+      CHECK(i1 == i0 + 1);
+      CHECK(slot_layout(nb, 1, probe, true).end > slot);  // really too long for the slot
+      check_layout(slot, 0, 1, probe, true);             // its record and offsets still fit
+    } else {
+      check_layout(slot, nb, i1 - i0, probe, true);
+      if (i1 < n) CHECK(slot_layout(off[i1 + 1] - off[i0], i1 + 1 - i0, probe, true).end > slot);  // maximal
+    }
+    i0 = i1;
+    ++chunks;
+  }
+  CHECK(i0 == n);
+}
+
+static void test_var_chunks() {
+  std::mt19937_64 rng(5);
+  const size_t slot = (size_t)1 << 20;
+  for (int probe = 0; probe < 2; ++probe) {
+    // U[8,512] keys, zero-length keys, one key of every size around the slot
+    std::vector<uint64_t> off{0};
+    for (int i = 0; i < 20000; ++i) off.push_back(off.back() + 8 + rng() % 505);
+    walk_var(off, slot, probe);
+    std::vector<uint64_t> zeros(100001, 123);  // 100000 empty keys starting at byte 123
+    walk_var(zeros, slot, probe);
+    for (uint64_t big : {slot - 1024, slot - 256, slot, slot + 1, (uint64_t)0x7fffffff}) {
+      std::vector<uint64_t> o{0, 10, 10 + big, 20 + big, 20 + big, 21 + big};
+      walk_var(o, slot, probe);
+    }
+    // lengths at the reference's limit, batches whose byte total passes 2^32 (only offsets are read)
+    std::vector<uint64_t> huge{0};
+    for (int i = 0; i < 5; ++i) huge.push_back(huge.back() + 0x7fffffffu);
+    walk_var(huge, slot, probe);
+    std::vector<uint64_t> one{(uint64_t)1 << 40, ((uint64_t)1 << 40) + 7};
+    walk_var(one, kMinSlotBytes, probe);
+  }
+}
+
+static void test_page_split() {
+  const uint64_t P = 4096;
+  // a buffer shorter than a page: nothing to lock
+  CHECK(!page_split(0x10000 + 16, 16, 100, 0x200000 + 16, P, 1).ok);
+  // ordinary case: whole pages inside both ranges, the keys they carry
+  {
+    const uint64_t kb = 0x1000010, ob = 0x9000030, n = 1000003, L = 16;
+    const PageSplit r = page_split(kb, L, n, ob, P, 1);
+    CHECK(r.ok);
+    CHECK(r.kp0 % P == 0 && r.kp1 % P == 0 && r.op0 % P == 0 && r.op1 % P == 0);
+    CHECK(r.kp0 >= kb && r.kp1 <= kb + n * L && r.op0 >= ob && r.op1 <= ob + n * 16);
+    CHECK(kb + r.lo * L >= r.kp0 && kb + r.hi * L <= r.kp1);   // keys [lo, hi) inside the locked key pages
+    CHECK(ob + r.lo * 16 >= r.op0 && ob + r.hi * 16 <= r.op1);  // records too
+    CHECK(kb + (r.lo - 1) * L < r.kp0 || ob + (r.lo - 1) * 16 < r.op0);  // lo is the first such key
+    CHECK(kb + (r.hi + 1) * L > r.kp1 || ob + (r.hi + 1) * 16 > r.op1);  // hi the last
+  }
+  // key pages and hash pages overlapping (records written over their own keys): refused
+  CHECK(!page_split(0x100000, 16, 100000, 0x100000 + 8192, P, 1).ok);
+  CHECK(!page_split(0x100000, 16, 100000, 0x100000, P, 1).ok);
+  // keys of odd lengths, every alignment
+  for (uint32_t L : {1u, 3u, 15u, 17u, 129u, 4097u})
+    for (uint64_t a = 0; a < 64; a += 7) {
+      const uint64_t kb = 0x40000000 + a, ob = 0x80000000 + 3 * a, n = 70000;
+      const PageSplit r = page_split(kb, L, n, ob, P, 1);
+      if (!r.ok) continue;
+      CHECK(kb + r.lo * L >= r.kp0 && kb + r.hi * (uint64_t)L <= r.kp1);
+      CHECK(ob + r.lo * 16 >= r.op0 && ob + r.hi * 16 <= r.op1);
+    }
+  // the 2^31-byte limit: a batch of 2^31-byte keys, and ranges that would wrap the address space
+  CHECK(!page_split(0x1000, 0x7fffffffu, 4, 0x7f0000000000, P, 1).ok);  // 64 B of records: no whole page
+  {
+    const PageSplit r = page_split(0x1000, 0x7fffffffu, 300, 0x7f0000000000, P, 1);
+    CHECK(r.ok && r.lo == 0 && r.hi == 256);  // the records' one whole page bounds the range
+  }
+  CHECK(!page_split(UINT64_MAX - 100, 16, 1000, 0x1000, P, 1).ok);
+  CHECK(!page_split(0x1000, 0x7fffffffu, (uint64_t)1 << 40, 0x2000, P, 1).ok);
+  CHECK(!page_split(0x1000, 0, 100, 0x100000, P, 1).ok);  // zero-length keys: nothing to read
+  CHECK(!page_split(0x100000, 16, 1000000, 0x10000000, 3000, 1).ok);  // not a power-of-two page
+  // fewer keys than the minimum
+  CHECK(!page_split(0x100000, 16, 1000000, 0x10000000, P, 2000000).ok);
+}
+
+// The pool under 16 threads: never more than max_slots slots alive, never one
+// slot lent twice, sizes changed while slots are on loan, failing allocations.
+struct FakeSlot {
+  size_t bytes = 0;
+  std::atomic<int> owners{0};
+  char* mem = nullptr;
+};
+
+static void test_pool() {
+  std::atomic<int> alive{0}, peak{0}, made{0}, fail_next{0};
+  SlotPool<FakeSlot> pool(
+      [&](size_t bytes, FakeSlot** out) {
+        if (fail_next.exchange(0)) return -4;
+        FakeSlot* s = new FakeSlot();
+        s->bytes = bytes;
+        s->mem = (char*)malloc(bytes);
+        memset(s->mem, 0, bytes);
+        const int a = ++alive;
+        int p = peak.load();
+        while (a > p && !peak.compare_exchange_weak(p, a)) {
+        }
+        ++made;
+        *out = s;
+        return 0;
+      },
+      [&](FakeSlot* s) {
+        CHECK(s->owners.load() == 0);
+        free(s->mem);
+        delete s;
+        --alive;
+      });
+  const int kMax = 4;
+  std::vector<std::thread> ts;
+  std::atomic<int> errors{0};
+  for (int t = 0; t < 16; ++t)
+    ts.emplace_back([&, t] {
+      std::mt19937 rng(t);
+      for (int it = 0; it < 400; ++it) {
+        FakeSlot* got[4] = {};
+        int n = 0;
+        const size_t bytes = (it / 100 % 2) ? 8192 : 4096;  // sizes change while others hold slots
+        if (t == 3 && it % 50 == 0) fail_next = 1;
+        const int rc = pool.acquire(bytes, 1 + rng() % 4, kMax, got, &n);
+        if (rc) {
+          ++errors;
+          CHECK(n == 0);
+          continue;
+        }
+        CHECK(n >= 1 && n <= 4);
+        for (int i = 0; i < n; ++i) {
+          CHECK(got[i]->bytes == bytes);
+          CHECK(got[i]->owners.fetch_add(1) == 0);  // lent to nobody else
+          got[i]->mem[rng() % bytes] = (char)t;      // ASan: inside the slot's arena
+        }
+        std::this_thread::yield();
+        for (int i = 0; i < n; ++i) got[i]->owners.fetch_sub(1);
+        pool.release(got, n);
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(peak.load() <= kMax);
+  CHECK(pool.live() == alive.load());
+  CHECK(pool.live() <= kMax);
+  pool.trim();
+  CHECK(alive.load() == 0 && pool.live() == 0);
+  // a smaller cap after use: extra slots are freed as they come back
+  FakeSlot* got[4] = {};
+  int n = 0;
+  CHECK(pool.acquire(4096, 4, 4, got, &n) == 0 && n == 4);
+  pool.release(got, 2);
+  FakeSlot* one[4] = {};
+  int m = 0;
+  CHECK(pool.acquire(4096, 4, 1, one, &m) == 0 && m >= 1);  // idle slots are lent even above the new cap
+  pool.release(got + 2, 2);
+  pool.release(one, m);
+  CHECK(pool.live() <= 1);
+  pool.trim();
+  CHECK(alive.load() == 0);
+  printf("pool: %d slots made, peak %d alive, %d injected failures\n", made.load(), peak.load(), errors.load());
+}
+
+int main() {
+  test_fixed_chunks();
+  test_var_chunks();
+  test_page_split();
+  test_pool();
+  if (failures) {
+    fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  printf("host_plan: all checks passed\n");
+  return 0;
+}

@@ -69,6 +69,26 @@ def test_seam_program_put_and_probed_get():
     assert r["win_range_put"] == r["n_put"]  # four window ranges, one handle each, put every key
 
 
+@pytest.mark.gpu
+def test_seam_program_under_host_sanitizers():
+    """The same seam program built with gcc -fsanitize=address,undefined (host
+    code only: the GPU kernels are the prebuilt library's), on a smaller batch:
+    the seam header's batching, window ranges and TLS hand-over under ASan/UBSan
+    (VERDICT r4 item 5). The HIP runtime's own allocations are not leak-checked."""
+    exe = os.path.join(ROOT, "tests", "c", "build", "test_seam_asan")
+    if not os.path.exists(exe):
+        pytest.skip("tests/c/build/test_seam_asan not built (needs /root/reference headers at build time)")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:protect_shadow_gap=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    p = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=300, env=env)
+    text = p.stdout + p.stderr
+    assert "ERROR: AddressSanitizer" not in text and "runtime error:" not in text, text
+    assert p.returncode == 0, text
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["ref_found"] == r["n_put"] == r["ref_right"] == r["probed_found"] == 20000
+    assert r["win_range_put"] == r["n_put"]
+
+
 # ---- the C++ seam: include/shf_hash_batch_shf.hpp through the reference's SharedHashFile class ----
 BIN_CPP = os.path.join(ROOT, "tests", "c", "build", "test_seam_cpp")
 

@@ -444,3 +444,68 @@ def test_fused_sync_host_var_and_device(hb, dev, oracle):
         assert hb.load().shf_hash_batch_var_win(vp(d), vp(ob), n, 12345, vp(out), vp(p), None, hb.MEM_DEVICE) \
             == hb.ERR_ARG
         assert hb.load().shf_hash_batch_fixed_win(vp(d), 16, 100, 12345, vp(out), vp(p), None, 9) == hb.ERR_ARG
+
+
+@pytest.mark.gpu
+def test_host_order_after_workspace_growth(hb, dev, oracle):
+    """The synchronous host-memory order keeps its device perm buffer across a
+    growth of the window-order workspace (the growth once freed the
+    perm buffer too, leaving a dangling pointer that the next smaller host call
+    wrote through). Host order of n1 keys, then a larger shf_win_order (grows the
+    workspace), then host orders of smaller and larger batches."""
+    rng = np.random.default_rng(77)
+    for n, grow in ((50_000, 400_000), (20_000, 1_600_000), (30_000, 0), (900_000, 0)):
+        keys = rng.integers(0, 256, size=n * 16, dtype=np.uint8)
+        want = oracle.hash_fixed(keys, 16)
+        h, perm, start = hb.hash_fixed_win_host(keys.reshape(n, 16))
+        np.testing.assert_array_equal(h, want)
+        ref_perm, ref_start = Oracle.win_order(want)
+        np.testing.assert_array_equal(perm, ref_perm)
+        np.testing.assert_array_equal(start, ref_start)
+        if grow:
+            g = _rand_hashes(grow, grow)
+            gp, gs = hb.win_order_host(g)
+            np.testing.assert_array_equal(gp, Oracle.win_order(g)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["fixed", "var", "fixed_win", "var_win"])
+def test_sync_device_calls_follow_the_default_stream(hb, dev, oracle, kind):
+    """Synchronous device-memory entry points run after the caller's work on the
+    null (torch default) stream: the keys are produced there by a long chain of
+    kernels and the call is made with no synchronize in between."""
+    import ctypes
+
+    import torch
+
+    n, L = 2_000_000, 16
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    lib = hb.load()
+    with torch.cuda.device(dev):
+        assert torch.cuda.current_stream(dev).cuda_stream == 0
+        base = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+        keys = torch.zeros_like(base)
+        torch.cuda.synchronize(dev)
+        want = oracle.hash_fixed(base.cpu().numpy(), L)
+        for _ in range(20):  # keep the default stream busy well past the call's launch
+            keys.copy_(base)
+            keys.add_(1)
+            keys.sub_(1)
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        off = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device=dev)
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        start = torch.empty(257, dtype=torch.int32, device=dev)
+        if kind == "fixed":
+            rc = lib.shf_hash_batch_fixed(vp(keys), L, n, 12345, vp(out), hb.MEM_DEVICE)
+        elif kind == "var":
+            rc = lib.shf_hash_batch_var(vp(keys), vp(off), n, 12345, vp(out), hb.MEM_DEVICE)
+        elif kind == "fixed_win":
+            rc = lib.shf_hash_batch_fixed_win(vp(keys), L, n, 12345, vp(out), vp(perm), vp(start), hb.MEM_DEVICE)
+        else:
+            rc = lib.shf_hash_batch_var_win(vp(keys), vp(off), n, 12345, vp(out), vp(perm), vp(start), hb.MEM_DEVICE)
+    assert rc == 0
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), want)
+    if kind.endswith("_win"):
+        ref_perm, ref_start = Oracle.win_order(want)
+        np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), ref_perm)
+        np.testing.assert_array_equal(start.cpu().numpy().view(np.uint32), ref_start)
