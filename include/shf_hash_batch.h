@@ -33,9 +33,10 @@
  *     64 MiB of device and 64 MiB of pinned memory per device, whatever the
  *     number of threads; slots of SHF_HB_STAGE_MB, default 16 MiB); a call
  *     borrows 1..SHF_HB_SLOTS (default 4) of them and waits only while every
- *     slot is on loan. Each thread keeps one HIP stream and a few status
- *     words per device, released when it exits (the main thread:
- *     shf_hash_batch_release()). Device selection follows the calling
+ *     slot is on loan. Each thread holds one HIP stream and a few status
+ *     words per device; when it exits they are kept for the next thread
+ *     (no HIP call runs at thread exit), and shf_hash_batch_release() frees
+ *     them. Device selection follows the calling
  *     thread's current HIP device (hipSetDevice), as HIP itself does.
  *   - Key lengths follow the reference's `const int len` parameter
  *     (murmurhash3.c:75): key_len and every variable key length must be
@@ -77,7 +78,7 @@ extern "C" {
 
 /* Where the caller's buffers live. */
 #define SHF_HASH_MEM_DEVICE 0 /* keys, offsets and out are device (HBM) pointers */
-#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); staged through the process's pinned slots, or read and written by the kernel in place (page-locked fixed-length buffers) */
+#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); staged through the process's pinned slots, or read and written by the kernel in place (fixed-length keys: page-locked caller buffers, and the whole pages of pageable ones, SHF_HB_PAGEABLE_ZERO_COPY=0 turns the latter off) */
 
 /* One result record: identical bytes to SHF_HASH (shf.private.h:180-185). */
 typedef struct shf_hash128 {
@@ -396,9 +397,9 @@ SHF_HB_API int shf_hash_batch_device_count(void);          /* visible HIP device
 SHF_HB_API int shf_hash_batch_check_device(void);          /* SHF_HB_OK if the current device can run the kernels */
 SHF_HB_API int shf_hash_batch_last_hip_error(void);        /* last hipError_t seen by this thread */
 /* Frees the calling thread's per-device state (stream, status words, window-order
- * buffers) and every idle staging slot of the process's pools; slots other
- * threads have on loan are kept. Other threads' state goes when they exit; the
- * main thread's only here. Any later call starts afresh. */
+ * buffers), the state exited threads left for reuse, and every idle staging slot
+ * of the process's pools; what other live threads hold is kept. Any later call
+ * starts afresh. */
 SHF_HB_API int shf_hash_batch_release(void);
 SHF_HB_API const char *shf_hash_batch_strerror(int status);
 SHF_HB_API const char *shf_hash_batch_version(void);

@@ -12,8 +12,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <sys/syscall.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -235,15 +233,25 @@ struct DevCtx {
 
 void release_ctx(DevCtx* c);
 
-// The calling thread's contexts, one per device, freed when the thread exits.
-// Not on the main thread at process exit (the HIP runtime may already be going
-// away, and the process's memory goes with it anyway): the main thread calls
-// shf_hash_batch_release() for that.
+// Contexts of threads that have exited, per device, kept for the next thread
+// that needs one: a thread's exit makes no HIP call (the runtime's own
+// per-thread state may already be gone by then, and freeing pinned memory from
+// a thread-exit handler is the one pattern this library does not trust), and
+// short-lived threads reuse a few contexts instead of making and freeing their
+// own. shf_hash_batch_release() frees the idle ones.
+std::mutex g_ctx_mu;
+std::map<int, std::vector<DevCtx*>> g_ctx_idle;
+
+void park_ctx(DevCtx* c) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  g_ctx_idle[c->dev].push_back(c);
+}
+
+// The calling thread's contexts, one per device; parked for reuse when it exits.
 struct ThreadCtxs {
   std::map<int, DevCtx*> m;
   ~ThreadCtxs() {
-    if ((pid_t)syscall(SYS_gettid) == getpid()) return;
-    for (auto& kv : m) release_ctx(kv.second);
+    for (auto& kv : m) park_ctx(kv.second);
     m.clear();
   }
 };
@@ -268,14 +276,28 @@ int current_ctx(DevCtx** out) {
     *out = it->second;
     return it->second->status;
   }
-  DevCtx* c = new DevCtx();
-  c->dev = dev;
-  c->status = check_arch(dev);
-  if (c->status == SHF_HB_OK) c->status = map_hip(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 3 * sizeof(uint32_t)));
-  if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
-  if (c->status == SHF_HB_OK)
-    c->status = map_hip(hipHostMalloc((void**)&c->h_status, sizeof(uint32_t), hipHostMallocDefault));
+  DevCtx* c = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    auto& idle = g_ctx_idle[dev];
+    if (!idle.empty()) {
+      c = idle.back();
+      idle.pop_back();
+    }
+  }
+  if (c) {  // an exited thread's context: its work is done once its stream is idle; fresh status words
+    (void)hipStreamSynchronize(c->st);
+    c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
+  } else {
+    c = new DevCtx();
+    c->dev = dev;
+    c->status = check_arch(dev);
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipMalloc((void**)&c->d_status, 3 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK) c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK)
+      c->status = map_hip(hipHostMalloc((void**)&c->h_status, sizeof(uint32_t), hipHostMallocDefault));
+  }
   tls_ctx.m[dev] = c;
   *out = c;
   return c->status;
@@ -296,12 +318,25 @@ void release_ctx(DevCtx* c) {
   delete c;
 }
 
-// Release every context of this thread now (the *_multi workers before they
-// report back, and shf_hash_batch_release(); other threads are covered by
-// ThreadCtxs at thread exit).
+// Hand this thread's contexts back now (the *_multi workers before they report
+// back); they are parked for the next thread, as at thread exit.
 void release_thread_ctx() {
-  for (auto& kv : tls_ctx.m) release_ctx(kv.second);
+  for (auto& kv : tls_ctx.m) park_ctx(kv.second);
   tls_ctx.m.clear();
+}
+
+// Frees this thread's contexts and every parked one (shf_hash_batch_release()).
+void free_contexts() {
+  release_thread_ctx();
+  std::vector<DevCtx*> all;
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    for (auto& kv : g_ctx_idle) {
+      all.insert(all.end(), kv.second.begin(), kv.second.end());
+      kv.second.clear();
+    }
+  }
+  for (DevCtx* c : all) release_ctx(c);
 }
 
 // shf_win_order's workspace: grown when a batch needs more, else reused (a hipFree per call
@@ -785,21 +820,23 @@ struct PageLock {
 // the range only partly covers go through the staged pipeline. A partial page
 // is never locked, so calls over neighbouring parts of one buffer (the
 // *_multi shards) never lock, or unlock, a page the other one uses.
-// Opt-in (SHF_HB_PAGEABLE_ZERO_COPY=1) since round 4: in 2 of 2 full GPU test
-// runs with it on by default, a later pageable hipMemcpy of the test process
-// (torch's .to(device) of a numpy array) failed with an illegal address, and
-// with it off 204 of 204 tests passed: registering and
-// unregistering ranges of the caller's pageable memory appears to leave the
-// runtime's own pageable-copy path a stale mapping. The product must not make a
-// caller's unrelated copies fault, so the default is the staged pipeline.
+// SHF_HB_PAGEABLE_ZERO_COPY=0 turns it off (read per call).
+// Round 4 saw two full GPU test runs with it on fail in a later pageable copy
+// of the test process (hipErrorIllegalAddress); tools/pageable_register_repro.hip
+// shows that exact failure comes from a registration that outlives the memory
+// it covers (scenario D), and that the lock / unlock / free / reuse cycle used
+// here leaves nothing behind (scenarios A-C). So every lock here is checked
+// both ways: pages the runtime already resolves are never locked, and an
+// unlock the runtime did not honour fails the call and turns the path off for
+// the process (g_lock_leaks). DESIGN.md §5.
 // Returns 1 when it does not apply (then nothing was launched).
 constexpr uint64_t kPage = 4096;
 constexpr uint64_t kPageableZeroCopyMin = (uint64_t)1 << 16;  // keys: below this, locking pages costs more
 
 int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                   const HostJob& job) {
-  const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");  // opt-in: "1"
-  if (!(e && e[0] == '1') || n < kPageableZeroCopyMin || g_lock_leaks.load()) return 1;
+  const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");  // "0": off
+  if ((e && e[0] == '0') || n < kPageableZeroCopyMin || g_lock_leaks.load()) return 1;
   // keys [lo, hi): every byte in [kp0, kp1) and every record in [op0, op1) (host_plan.h)
   const shfhb::plan::PageSplit ps = shfhb::plan::page_split(reinterpret_cast<uintptr_t>(keys), key_len, n,
                                                             reinterpret_cast<uintptr_t>(job.hash), kPage,
@@ -1653,7 +1690,7 @@ int shf_hash_batch_check_device(void) {
 int shf_hash_batch_last_hip_error(void) { return tls_last_hip; }
 
 int shf_hash_batch_release(void) {
-  release_thread_ctx();
+  free_contexts();
   std::vector<Pool*> pools;
   {
     std::lock_guard<std::mutex> g(g_pools_mu);
