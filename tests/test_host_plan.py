@@ -7,6 +7,7 @@
   hash pages overlapping, key lengths and batches at the 2^31-byte limit of the
   reference's `const int len` (/root/reference/src/murmurhash3.c:75), 16 threads
   borrowing slots while the slot size changes and allocations fail;
+* the same program under ThreadSanitizer (the pool's locking);
 * tests/c/test_oracle_asan.c: the C oracle against every golden the reference
   produced (tests/golden/murmur3_golden.json), each key in a buffer of exactly
   its length so a tail over-read is a sanitizer report;
@@ -46,6 +47,14 @@ def test_host_plan_under_sanitizers(built):
     p = subprocess.run([os.path.join(built, "test_host_plan_asan")], capture_output=True, text=True, timeout=300,
                        env=SAN_ENV)
     _no_reports(p)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "all checks passed" in p.stdout
+
+
+def test_host_plan_pool_under_thread_sanitizer(built):
+    p = subprocess.run([os.path.join(built, "test_host_plan_tsan")], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert "WARNING: ThreadSanitizer" not in p.stdout + p.stderr, p.stderr
     assert p.returncode == 0, p.stdout + p.stderr
     assert "all checks passed" in p.stdout
 
