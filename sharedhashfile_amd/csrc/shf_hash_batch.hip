@@ -286,8 +286,10 @@ int current_ctx(DevCtx** out) {
     }
   }
   if (c) {  // an exited thread's context: its work is done once its stream is idle; fresh status words
-    (void)hipStreamSynchronize(c->st);
-    c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
+    if (c->status == SHF_HB_OK) {  // (a context that failed to start keeps its error)
+      (void)hipStreamSynchronize(c->st);
+      c->status = map_hip(hipMemset(c->d_status, 0, 3 * sizeof(uint32_t)));
+    }
   } else {
     c = new DevCtx();
     c->dev = dev;
