@@ -431,12 +431,16 @@ def test_host_var_kernel_by_mean_length(hb, dev, oracle, lo, hi):
     assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
 
 
-@pytest.mark.parametrize("stage_mb,slots", [(1, 2), (1, 4), (3, 3), (64, 2)])
-def test_host_pipeline_shapes(hb, dev, oracle, monkeypatch, stage_mb, slots):
-    """SHF_HB_STAGE_MB / SHF_HB_SLOTS change only how a host batch is chunked
-    and overlapped (many chunks, a key larger than a chunk)."""
+@pytest.mark.parametrize("stage_mb,slots,pool_mb", [(1, 2, 64), (1, 4, 64), (3, 3, 64), (64, 2, 256), (1, 4, 1),
+                                                    (16, 4, 16), (2, 1, 64), (16, 4, 8)])
+def test_host_pipeline_shapes(hb, dev, oracle, monkeypatch, stage_mb, slots, pool_mb):
+    """SHF_HB_STAGE_MB / SHF_HB_SLOTS / SHF_HB_POOL_MB change only how a host
+    batch is chunked and overlapped (many chunks, a key larger than a slot),
+    down to a pool of one slot (pool smaller than one slot: still one)."""
     monkeypatch.setenv("SHF_HB_STAGE_MB", str(stage_mb))
     monkeypatch.setenv("SHF_HB_SLOTS", str(slots))
+    monkeypatch.setenv("SHF_HB_POOL_MB", str(pool_mb))
+    monkeypatch.setenv("SHF_HB_PAGEABLE_ZERO_COPY", "0")  # every key through the slots
     n = 600_000
     flat = np.frombuffer(splitmix_bytes(n * 16, 31), dtype=np.uint8)
     assert np.array_equal(hb.hash_fixed_host(flat, 16), oracle.hash_fixed(flat, 16, threads=8))

@@ -230,6 +230,46 @@ def test_concurrent_threads_share_the_staging_pool(hb, dev, oracle):
     assert torch.cuda.mem_get_info()[0] >= free0 - (8 << 20)
 
 
+@pytest.mark.parametrize("pool_mb", ["1", "32"])
+def test_threads_wait_for_slots_of_a_small_pool(hb, dev, oracle, monkeypatch, pool_mb):
+    """8 threads, fixed- and variable-length host batches at once, through a
+    pool of one slot (1 MiB: less than one 16-MiB slot still makes one) or two:
+    a call waits only for its first slot, none waits while holding one, and
+    every result is bit-exact."""
+    monkeypatch.setenv("SHF_HB_POOL_MB", pool_mb)
+    monkeypatch.setenv("SHF_HB_PAGEABLE_ZERO_COPY", "0")
+    lib = hb.load()
+    n = 1_500_007
+    keys = np.frombuffer(splitmix_bytes(n * 16, 81), dtype=np.uint8)
+    want = oracle.hash_fixed(keys, 16, threads=8)
+    rng = np.random.default_rng(82)
+    m = 150_001
+    lens = rng.integers(0, 600, size=m)
+    off = np.zeros(m + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    vwant = oracle.hash_var(data, off)
+    ok = []
+
+    def call(i):
+        if i % 2:
+            out = np.empty((n, 2), dtype=np.uint64)
+            rc = lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, 12345, out.ctypes.data, hb.MEM_HOST)
+            ok.append(rc == 0 and np.array_equal(out, want))
+        else:
+            out = np.empty((m, 2), dtype=np.uint64)
+            rc = lib.shf_hash_batch_var(data.ctypes.data, off.ctypes.data, m, 12345, out.ctypes.data, hb.MEM_HOST)
+            ok.append(rc == 0 and np.array_equal(out, vwant))
+
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts), "a call never got a slot"
+    assert ok == [True] * 8
+
+
 @pytest.mark.parametrize("n_devices", [2, 3])
 def test_multi_split_with_shared_device(hb, dev, oracle, monkeypatch, n_devices):
     """shf_hash_batch_*_multi's split (one host thread per shard, contiguous key
