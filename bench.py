@@ -873,9 +873,8 @@ def time_host_inclusive(args, dev):
                                      "timed repeats after one untimed call; *_pinned = page-locked caller buffers "
                                      "(16-B keys: the kernel reads and writes them over PCIe, zero copy), "
                                      "*_pinned_staged = the same through hipMemcpyAsync both ways; "
-                                     "fixed16_pageable = pageable buffers, the library's default (their whole pages "
-                                     "locked for the call and read / written by the kernel), *_pageable_staged and "
-                                     "var_pageable = pageable buffers through the staged pipeline"
+                                     "*_pageable = pageable buffers through the staged pipeline (the library never "
+                                     "page-locks a caller's pageable memory)"
                                      % n}
 
     def _staged(fn, var="SHF_HB_ZERO_COPY_MAX_KEY"):  # through the copy-engine pipeline (zero copy off)
@@ -906,8 +905,6 @@ def time_host_inclusive(args, dev):
     cases = [
         ("fixed16_pageable", lambda: lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, SEED, out.ctypes.data,
                                                               hb.MEM_HOST), 5),
-        ("fixed16_pageable_staged", lambda: _staged(lambda: lib.shf_hash_batch_fixed(
-            keys.ctypes.data, 16, n, SEED, out.ctypes.data, hb.MEM_HOST), "SHF_HB_PAGEABLE_ZERO_COPY"), 5),
         ("fixed16_pinned", lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED, po.data_ptr(), hb.MEM_HOST),
          5),
         ("fixed16_pinned_staged", lambda: _staged(lambda: lib.shf_hash_batch_fixed(pk.data_ptr(), 16, n, SEED,

@@ -5,8 +5,6 @@
 //   * slot_layout / fixed_chunk_keys / var_chunk_end: how one chunk of keys, its
 //     hash records, probe records and offsets are carved out of one staging slot
 //     (a pinned host arena and a device arena of the same size);
-//   * page_split: which whole pages of a pageable caller buffer the pageable
-//     zero copy may page-lock, and which keys they carry;
 //   * SlotPool: the per-device pool of staging slots that every calling thread
 //     borrows from (a bounded footprint per process, not per thread).
 //
@@ -88,38 +86,6 @@ inline uint64_t var_chunk_end(const uint64_t* offsets, uint64_t i0, uint64_t n, 
       hi = mid - 1;
   }
   return lo;
-}
-
-// Pageable zero copy (shf_hash_batch.hip host_fixed_pageable_zero_copy): the
-// whole pages [kp0, kp1) inside the keys' bytes [kb, kb + n * key_len) and
-// [op0, op1) inside the records [ob, ob + 16 n), and the keys [lo, hi) whose
-// bytes and record lie wholly in those pages. ok = false when there is no such
-// range of at least min_keys keys, the two page ranges overlap, or the ranges
-// do not fit the address space.
-struct PageSplit {
-  bool ok = false;
-  uint64_t kp0 = 0, kp1 = 0, op0 = 0, op1 = 0, lo = 0, hi = 0;
-};
-
-inline PageSplit page_split(uint64_t kb, uint32_t key_len, uint64_t n, uint64_t ob, uint64_t page,
-                            uint64_t min_keys) {
-  PageSplit r;
-  uint64_t kbytes = 0, obytes = 0, kend = 0, oend = 0;
-  if (!key_len || !n || !page || (page & (page - 1))) return r;
-  if (__builtin_mul_overflow(n, (uint64_t)key_len, &kbytes) || __builtin_mul_overflow(n, (uint64_t)kHashBytes, &obytes) ||
-      __builtin_add_overflow(kb, kbytes, &kend) || __builtin_add_overflow(ob, obytes, &oend) || kb > UINT64_MAX - page ||
-      ob > UINT64_MAX - page)
-    return r;
-  r.kp0 = (kb + page - 1) & ~(page - 1);
-  r.kp1 = kend & ~(page - 1);
-  r.op0 = (ob + page - 1) & ~(page - 1);
-  r.op1 = oend & ~(page - 1);
-  if (r.kp1 <= r.kp0 || r.op1 <= r.op0) return r;
-  if (r.kp1 > r.op0 && r.op1 > r.kp0) return r;  // key and record pages overlap
-  r.lo = std::max((r.kp0 - kb + key_len - 1) / key_len, (r.op0 - ob + kHashBytes - 1) / kHashBytes);
-  r.hi = std::min((r.kp1 - kb) / key_len, (r.op1 - ob) / kHashBytes);
-  r.ok = r.hi > r.lo && r.hi - r.lo >= min_keys;
-  return r;
 }
 
 // A bounded pool of staging slots, shared by every thread of the process that

@@ -14,7 +14,6 @@
 
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -373,24 +372,6 @@ int ensure_perm(DevCtx* c, uint64_t n, uint32_t** out) {
   return SHF_HB_OK;
 }
 
-// Pages this library page-locks for the length of one call
-// (host_fixed_pageable_zero_copy). Another thread's call over the same caller
-// buffer neither locks them again (PageLock::lock refuses any overlap) nor
-// takes them for the caller's own page-locked memory (is_host_pinned), which
-// would have its copies or kernel still reading them over PCIe when the first
-// call unlocks them. An entry is made before the pages are locked and removed
-// after they are unlocked, so a lookup that sees them locked always finds it.
-std::mutex g_lib_lock_mu;
-std::vector<std::pair<uintptr_t, uintptr_t>> g_lib_locks;  // [start, end)
-
-bool library_locked(const void* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  std::lock_guard<std::mutex> g(g_lib_lock_mu);
-  for (const auto& r : g_lib_locks)
-    if (a >= r.first && a < r.second) return true;
-  return false;
-}
-
 // Caller host memory that is already page-locked (hipHostMalloc /
 // hipHostRegister by the caller): DMA straight from / into it, no staging copy.
 bool is_host_pinned(const void* p) {
@@ -400,7 +381,7 @@ bool is_host_pinned(const void* p) {
     (void)hipGetLastError();  // pageable memory: clear the sticky error
     return false;
   }
-  return a.type == hipMemoryTypeHost && !library_locked(p);
+  return a.type == hipMemoryTypeHost;
 }
 
 // memcpy split over a few threads (SHF_HB_COPY_THREADS, default 8, read per
@@ -693,7 +674,7 @@ uint32_t zero_copy_max_key() {
 // Device address of host bytes [p, p + bytes), when they lie in one
 // page-locked allocation that the current device maps; else nullptr.
 void* host_range_device_ptr(const void* p, size_t bytes) {
-  if (!p || !bytes || library_locked(p)) return nullptr;  // another call's pages: not the caller's to use
+  if (!p || !bytes) return nullptr;
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   void* d = nullptr;
@@ -721,167 +702,27 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
   return j;
 }
 
-int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in,
-                   bool direct = true);
-HostJob hash_job(shf_hash128* out);
+// Pageable caller buffers are never page-locked by this library: they go
+// through the staged pipeline. Rounds 3-5 locked their whole interior pages
+// for a call (hipHostRegister) and let the kernel read and write them over
+// PCIe (2.38 against 2.03 G keys/s staged for 10M x 16-B keys); in 3 of the
+// last 5 full GPU test runs with that path on, a later pageable copy of the
+// same process (torch's .to(device) / .cpu() of a >= 1 MB buffer) failed with
+// hipErrorIllegalAddress, and in none of 6 with it off. A registration that
+// outlives its memory produces exactly that failure
+// (tools/pageable_register_repro.hip, scenario D); the lock / unlock / free /
+// reuse sequences the library used, replayed alone, do not (scenarios A-C, E),
+// even with every lock checked against the runtime both ways. The interaction lies inside the runtime's own
+// pageable-copy path; a library must not put its caller's unrelated copies at
+// risk for 15 %, so the path is gone.
 
-// SHF_HB_TRACE_LOCKS=1 (read once): every page lock and unlock of the pageable
-// zero copy is printed on stderr with its range and the runtime's answers.
-bool trace_locks() {
-  static const bool on = [] {
-    const char* e = getenv("SHF_HB_TRACE_LOCKS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// Does the runtime hold a registration covering host address p? (hipHostRegister'd or
-// hipHostMalloc'd: the runtime then resolves p to a device mapping for every copy and kernel.)
-bool runtime_registered(const void* p) {
-  hipPointerAttribute_t a;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return a.type == hipMemoryTypeHost;
-}
-
-// Registrations of caller pages this library failed to end (hipHostUnregister failed, or the
-// runtime still resolved the range afterwards). A registration that outlives the caller's
-// buffer gives the next buffer mapped at that address a stale device mapping: any pageable
-// copy from it then fails with hipErrorIllegalAddress (tools/pageable_register_repro.hip,
-// scenario D). Never expected to be non-zero; the pageable zero copy refuses to run once it is.
-std::atomic<int> g_lock_leaks{0};
-
-// Page-locks [p, p + bytes) (whole pages) for one call and unlocks it after.
-struct PageLock {
-  void* p = nullptr;
-  void* dev = nullptr;
-  size_t bytes = 0;
-  std::pair<uintptr_t, uintptr_t> range{0, 0};  // listed in g_lib_locks while non-empty
-  bool lock(void* at, size_t n) {
-    const std::pair<uintptr_t, uintptr_t> r{reinterpret_cast<uintptr_t>(at), reinterpret_cast<uintptr_t>(at) + n};
-    {
-      // pages another call of this library holds: leave them to it (concurrent hipHostRegister
-      // of one range, and unlocking under the other call's kernel, are both avoided)
-      std::lock_guard<std::mutex> g(g_lib_lock_mu);
-      for (const auto& o : g_lib_locks)
-        if (r.first < o.second && o.first < r.second) return false;
-      g_lib_locks.push_back(r);
-    }
-    range = r;
-    // pages the runtime already resolves (the caller's own registration): not ours to lock
-    if (runtime_registered(at) || runtime_registered(static_cast<uint8_t*>(at) + n - 1)) return false;
-    const hipError_t e = hipHostRegister(at, n, hipHostRegisterMapped);
-    if (trace_locks()) fprintf(stderr, "shf_hash_batch lock [%p, +%zu) -> %d\n", at, n, (int)e);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();  // e.g. pages another call (or the caller) has locked: not ours to use
-      return false;
-    }
-    p = at;
-    bytes = n;
-    if (hipHostGetDevicePointer(&dev, at, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    return true;
-  }
-  // Ends the registration; SHF_HB_ERR_HIP if the runtime still resolves the range after it.
-  int unlock() {
-    int rc = SHF_HB_OK;
-    if (p) {
-      const hipError_t e = hipHostUnregister(p);
-      if (e != hipSuccess) (void)hipGetLastError();
-      const bool still = runtime_registered(p) || runtime_registered(static_cast<uint8_t*>(p) + bytes - 1);
-      if (trace_locks())
-        fprintf(stderr, "shf_hash_batch unlock [%p, +%zu) -> %d%s\n", p, bytes, (int)e, still ? " STILL REGISTERED" : "");
-      if (e != hipSuccess || still) {
-        g_lock_leaks.fetch_add(1);
-        if (debug_errors()) fprintf(stderr, "shf_hash_batch: page lock [%p, +%zu) not ended (%d)\n", p, bytes, (int)e);
-        tls_last_hip = e != hipSuccess ? (int)e : (int)hipErrorHostMemoryAlreadyRegistered;
-        rc = SHF_HB_ERR_HIP;
-      }
-      p = nullptr;
-    }
-    if (range.second) {  // after the unlock (equal entries of other calls are interchangeable)
-      std::lock_guard<std::mutex> g(g_lib_lock_mu);
-      const auto it = std::find(g_lib_locks.begin(), g_lib_locks.end(), range);
-      if (it != g_lib_locks.end()) g_lib_locks.erase(it);
-      range = {0, 0};
-    }
-    return rc;
-  }
-  ~PageLock() { (void)unlock(); }
-};
-
-// Pageable caller buffers, zero copy. The pages that lie wholly inside the
-// caller's key range and inside its hash range are page-locked for this call
-// (hipHostRegister; per call: 10M x 16-B keys 1.75 vs 1.59 G keys/s staged,
-// profiles/r2/host_zero_copy/probe4.txt) and one kernel reads and writes them
-// over PCIe; the few keys at either end whose bytes or record touch a page
-// the range only partly covers go through the staged pipeline. A partial page
-// is never locked, so calls over neighbouring parts of one buffer (the
-// *_multi shards) never lock, or unlock, a page the other one uses.
-// SHF_HB_PAGEABLE_ZERO_COPY=0 turns it off (read per call).
-// Round 4 saw two full GPU test runs with it on fail in a later pageable copy
-// of the test process (hipErrorIllegalAddress); tools/pageable_register_repro.hip
-// shows that exact failure comes from a registration that outlives the memory
-// it covers (scenario D), and that the lock / unlock / free / reuse cycle used
-// here leaves nothing behind (scenarios A-C). So every lock here is checked
-// both ways: pages the runtime already resolves are never locked, and an
-// unlock the runtime did not honour fails the call and turns the path off for
-// the process (g_lock_leaks). DESIGN.md §5.
-// Returns 1 when it does not apply (then nothing was launched).
-constexpr uint64_t kPage = 4096;
-constexpr uint64_t kPageableZeroCopyMin = (uint64_t)1 << 16;  // keys: below this, locking pages costs more
-
-int host_fixed_pageable_zero_copy(DevCtx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed,
-                                  const HostJob& job) {
-  const char* e = getenv("SHF_HB_PAGEABLE_ZERO_COPY");  // "0": off
-  if ((e && e[0] == '0') || n < kPageableZeroCopyMin || g_lock_leaks.load()) return 1;
-  // keys [lo, hi): every byte in [kp0, kp1) and every record in [op0, op1) (host_plan.h)
-  const shfhb::plan::PageSplit ps = shfhb::plan::page_split(reinterpret_cast<uintptr_t>(keys), key_len, n,
-                                                            reinterpret_cast<uintptr_t>(job.hash), kPage,
-                                                            kPageableZeroCopyMin);
-  if (!ps.ok) return 1;
-  const uint64_t kb = reinterpret_cast<uintptr_t>(keys), ob = reinterpret_cast<uintptr_t>(job.hash);
-  const uint64_t lo = ps.lo, hi = ps.hi;
-  PageLock lk, lo_;
-  if (!lk.lock(reinterpret_cast<void*>(ps.kp0), ps.kp1 - ps.kp0) ||
-      !lo_.lock(reinterpret_cast<void*>(ps.op0), ps.op1 - ps.op0))
-    return 1;  // e.g. already page-locked by someone else: the staged pipeline instead
-  const uint8_t* dk = static_cast<const uint8_t*>(lk.dev) + (kb + lo * key_len - ps.kp0);
-  shf_hash128* dh = reinterpret_cast<shf_hash128*>(static_cast<uint8_t*>(lo_.dev) + (ob + lo * 16 - ps.op0));
-  shfhb::Sink mk;
-  int mmode = direct_sink(job, dh, &mk);
-  if (mk.wins) mk.wins += lo;
-  HB_TRY(shfhb::launch_fixed(dk, key_len, hi - lo, seed, mk, mmode, c->st, shfhb::kKernelAuto));
-  // the ends meanwhile, through the staged pipeline (on the pool's slots, beside the launch),
-  // copied through the staging as pageable memory: they may begin inside the pages just locked and
-  // run past them, so they must not be taken for page-locked buffers
-  int rc = SHF_HB_OK;
-  HostJob head = hash_job(job.hash), tail = hash_job(job.hash + hi);
-  head.wins = job.wins;
-  tail.wins = job.wins ? job.wins + hi : nullptr;
-  if (lo) rc = host_fixed_run(keys, key_len, lo, seed, head, false);
-  if (rc == SHF_HB_OK && hi < n) rc = host_fixed_run(keys + hi * key_len, key_len, n - hi, seed, tail, false);
-  const hipError_t se = hipStreamSynchronize(c->st);  // before the pages are unlocked
-  const int ru = lk.unlock(), rv = lo_.unlock();
-  if (rc) return rc;
-  HB_TRY(se);
-  return ru ? ru : rv;
-}
-
-// Host-memory fixed-length pipeline on the current device. direct = false: the
-// caller's buffers are staged as pageable memory whatever they are (no zero
-// copy, no DMA in place, no direct hash stores).
-int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in,
-                   bool direct) {
-  const HostJob job = direct ? with_direct_out(job_in, n) : job_in;
+// Host-memory fixed-length pipeline on the current device.
+int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in) {
+  const HostJob job = with_direct_out(job_in, n);
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  if (direct && job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
+  if (job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
     void* dk = host_range_device_ptr(keys, (size_t)n * key_len);
     void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)) : nullptr;
     if (dh) {
@@ -891,10 +732,6 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
       HB_TRY(hipStreamSynchronize(c->st));
       return SHF_HB_OK;
     }
-    if (!is_host_pinned(keys) && !is_host_pinned(job.hash)) {
-      rc = host_fixed_pageable_zero_copy(c, keys, key_len, n, seed, job);
-      if (rc != 1) return rc;
-    }
   }
   const bool probe = job.probe != nullptr;
   if (!shfhb::plan::fixed_chunk_keys(std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), key_len, probe))
@@ -903,8 +740,8 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   if ((rc = lease_slots(c->dev, pipeline_slots(), &L))) return rc;
   const uint64_t chunk = std::min<uint64_t>(shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe), n);
   const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false);
-  const bool in_pinned = direct && is_host_pinned(keys), hash_pinned = direct && is_host_pinned(job.hash),
-             probe_pinned = direct && is_host_pinned(job.probe);
+  const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
+             probe_pinned = is_host_pinned(job.probe);
   if (trace_on()) tls_trace.slots = L.n;
   Pending pend[kMaxSlots];
   uint64_t idx = 0;

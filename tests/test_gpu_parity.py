@@ -440,7 +440,6 @@ def test_host_pipeline_shapes(hb, dev, oracle, monkeypatch, stage_mb, slots, poo
     monkeypatch.setenv("SHF_HB_STAGE_MB", str(stage_mb))
     monkeypatch.setenv("SHF_HB_SLOTS", str(slots))
     monkeypatch.setenv("SHF_HB_POOL_MB", str(pool_mb))
-    monkeypatch.setenv("SHF_HB_PAGEABLE_ZERO_COPY", "0")  # every key through the slots
     n = 600_000
     flat = np.frombuffer(splitmix_bytes(n * 16, 31), dtype=np.uint8)
     assert np.array_equal(hb.hash_fixed_host(flat, 16), oracle.hash_fixed(flat, 16, threads=8))

@@ -237,7 +237,6 @@ def test_threads_wait_for_slots_of_a_small_pool(hb, dev, oracle, monkeypatch, po
     a call waits only for its first slot, none waits while holding one, and
     every result is bit-exact."""
     monkeypatch.setenv("SHF_HB_POOL_MB", pool_mb)
-    monkeypatch.setenv("SHF_HB_PAGEABLE_ZERO_COPY", "0")
     lib = hb.load()
     n = 1_500_007
     keys = np.frombuffer(splitmix_bytes(n * 16, 81), dtype=np.uint8)

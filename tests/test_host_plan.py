@@ -1,12 +1,12 @@
 """Host code under AddressSanitizer + UndefinedBehaviorSanitizer, on the CPU
 (SURVEY.md §5 plans ASan/UBSan for host code):
 
-* tests/c/test_host_plan.cpp: the host pipelines' chunk and page arithmetic and
-  the process staging pool (sharedhashfile_amd/csrc/host_plan.h, compiled into
-  the product library) -- edge ranges: a buffer shorter than a page, key and
-  hash pages overlapping, key lengths and batches at the 2^31-byte limit of the
-  reference's `const int len` (/root/reference/src/murmurhash3.c:75), 16 threads
-  borrowing slots while the slot size changes and allocations fail;
+* tests/c/test_host_plan.cpp: the host pipelines' chunk arithmetic and the
+  process staging pool (sharedhashfile_amd/csrc/host_plan.h, compiled into the
+  product library) -- edge ranges: slots shorter than one key, key lengths and
+  batches at the 2^31-byte limit of the reference's `const int len`
+  (/root/reference/src/murmurhash3.c:75), 16 threads borrowing slots while the
+  slot size changes and allocations fail;
 * the same program under ThreadSanitizer (the pool's locking);
 * tests/c/test_oracle_asan.c: the C oracle against every golden the reference
   produced (tests/golden/murmur3_golden.json), each key in a buffer of exactly

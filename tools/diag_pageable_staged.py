@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Where the pageable staged host path's spread comes from.
 
-Times shf_hash_batch_fixed(MEM_HOST) over pageable numpy buffers with zero copy
-off (SHF_HB_PAGEABLE_ZERO_COPY=0: the staged pipeline -- chunked par_memcpy into
+Times shf_hash_batch_fixed(MEM_HOST) over pageable numpy buffers (the staged
+pipeline, the only path for pageable memory since round 5 -- chunked par_memcpy into
 pinned staging, H2D, kernel, direct stores into pinned staging, drain copy),
 --repeats times, and records per repeat: wall time, minor page faults,
 voluntary / involuntary context switches, process CPU time, and the cgroup's
@@ -40,7 +40,6 @@ def main():
     p.add_argument("--env", action="append", default=[], help="NAME=VALUE set before the calls")
     p.add_argument("--trace-file", default=None, help="where this run's stderr goes (with SHF_HB_TRACE=1)")
     a = p.parse_args()
-    os.environ["SHF_HB_PAGEABLE_ZERO_COPY"] = "0"
     for kv in a.env:
         k, _, v = kv.partition("=")
         os.environ[k] = v
