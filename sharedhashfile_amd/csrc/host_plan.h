@@ -5,6 +5,7 @@
 //   * slot_layout / fixed_chunk_keys / var_chunk_end: how one chunk of keys, its
 //     hash records, probe records and offsets are carved out of one staging slot
 //     (a pinned host arena and a device arena of the same size);
+//   * stream_copy_avx2: the staging copies' non-temporal memcpy;
 //   * SlotPool: the per-device pool of staging slots that every calling thread
 //     borrows from (a bounded footprint per process, not per thread).
 //
@@ -13,8 +14,10 @@
 // variable-length batches are validated (offsets non-decreasing, lengths < 2^31)
 // before any of this runs (check_var_lengths_host).
 #pragma once
+#include <immintrin.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -86,6 +89,30 @@ inline uint64_t var_chunk_end(const uint64_t* offsets, uint64_t i0, uint64_t n, 
       hi = mid - 1;
   }
   return lo;
+}
+
+// memcpy with non-temporal 32-B stores (the CPU must have AVX2): head bytes up
+// to the destination's next 32-B boundary and the last n % 128 bytes by
+// memcpy, 128 B per step between them; an sfence at the end makes the streamed
+// lines visible before the caller hands the buffer on (a DMA, the caller).
+__attribute__((target("avx2"))) inline void stream_copy_avx2(void* dst, const void* src, size_t n) {
+  char* d = static_cast<char*>(dst);
+  const char* s = static_cast<const char*>(src);
+  const size_t head = std::min(n, (size_t)((32u - (reinterpret_cast<uintptr_t>(d) & 31u)) & 31u));
+  memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  for (size_t k = n / 128; k; --k, d += 128, s += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + 96), e);
+  }
+  memcpy(d, s, n & 127u);
+  _mm_sfence();
 }
 
 // A bounded pool of staging slots, shared by every thread of the process that

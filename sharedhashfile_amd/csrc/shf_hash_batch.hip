@@ -449,19 +449,38 @@ CopyPool& copy_pool() {
   return *p;
 }
 
+// Staging copies with non-temporal stores: the destination of every staging
+// copy is written once and not read back by this core soon (pinned staging the
+// device reads by DMA, or the caller's records), so streaming stores skip the
+// read-for-ownership a cached store pays and leave the caches to the caller.
+// SHF_HB_COPY_NT=0 (read per call) uses memcpy throughout.
+bool copy_nt() {
+  const char* e = getenv("SHF_HB_COPY_NT");
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  return avx2 && !(e && e[0] == '0');
+}
+
+void copy_piece(void* dst, const void* src, size_t n, bool nt) {
+  if (nt && n >= 4096)
+    shfhb::plan::stream_copy_avx2(dst, src, n);
+  else
+    memcpy(dst, src, n);
+}
+
 void par_memcpy(void* dst, const void* src, size_t n) {
   constexpr size_t kMinPerThread = (size_t)2 << 20;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t t = std::min<size_t>({copy_threads(), (size_t)hw, std::max<size_t>(1, n / kMinPerThread)});
+  const bool nt = copy_nt();
   if (t <= 1) {
-    memcpy(dst, src, n);
+    copy_piece(dst, src, n, nt);
     return;
   }
   const size_t per = (n + t - 1) / t;
   std::vector<std::function<void()>> pieces;
   for (size_t i = 0; i < t; ++i) {
     const size_t a = i * per, b = std::min(n, a + per);
-    if (a < b) pieces.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    if (a < b) pieces.emplace_back([=] { copy_piece((char*)dst + a, (const char*)src + a, b - a, nt); });
   }
   copy_pool().run(pieces);
 }

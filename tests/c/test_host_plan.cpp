@@ -111,6 +111,35 @@ static void test_var_chunks() {
   }
 }
 
+// The staging copies' streaming memcpy: every length 0..600 and some long ones,
+// at every source and destination offset within 64 B, into exact-size heap
+// buffers (ASan reports any byte written or read outside them).
+static void test_stream_copy() {
+  if (!__builtin_cpu_supports("avx2")) {
+    printf("stream_copy: no AVX2 on this CPU, skipped\n");
+    return;
+  }
+  std::mt19937 rng(9);
+  std::vector<size_t> lens;
+  for (size_t n = 0; n <= 600; ++n) lens.push_back(n);
+  for (size_t n : {4095, 4096, 4097, 65536 + 31, 1000003}) lens.push_back(n);
+  for (size_t n : lens)
+    for (size_t so = 0; so < 64; so += (n > 600 ? 13 : 5))
+      for (size_t dof = 0; dof < 64; dof += (n > 600 ? 11 : 7)) {
+        char* src = (char*)malloc(n + so + 1);
+        char* dst = (char*)malloc(n + dof + 1);
+        for (size_t i = 0; i < n + so + 1; ++i) src[i] = (char)rng();
+        memset(dst, 0x5a, n + dof + 1);
+        stream_copy_avx2(dst + dof, src + so, n);
+        CHECK(memcmp(dst + dof, src + so, n) == 0);
+        bool guard = dst[n + dof] == 0x5a;
+        for (size_t i = 0; i < dof; ++i) guard = guard && dst[i] == 0x5a;
+        CHECK(guard);  // nothing outside [dof, dof + n) written
+        free(src);
+        free(dst);
+      }
+}
+
 // The pool under 16 threads: never more than max_slots slots alive, never one
 // slot lent twice, sizes changed while slots are on loan, failing allocations.
 struct FakeSlot {
@@ -195,6 +224,7 @@ static void test_pool() {
 int main() {
   test_fixed_chunks();
   test_var_chunks();
+  test_stream_copy();
   test_pool();
   if (failures) {
     fprintf(stderr, "%d check(s) failed\n", failures);
