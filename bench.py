@@ -874,7 +874,8 @@ def time_host_inclusive(args, dev):
                                      "(16-B keys: the kernel reads and writes them over PCIe, zero copy), "
                                      "*_pinned_staged = the same through hipMemcpyAsync both ways; "
                                      "*_pageable = pageable buffers through the staged pipeline (the library never "
-                                     "page-locks a caller's pageable memory)"
+                                     "page-locks a caller's pageable memory); *_x16 = 16 threads, one slice each, "
+                                     "at once (one staging pool)"
                                      % n}
 
     def _staged(fn, var="SHF_HB_ZERO_COPY_MAX_KEY"):  # through the copy-engine pipeline (zero copy off)
@@ -887,6 +888,17 @@ def time_host_inclusive(args, dev):
                 os.environ.pop(var, None)
             else:
                 os.environ[var] = old
+    def _threaded(k, call):  # k threads over even slices of [0, n); the first failing status, else 0
+        import threading
+
+        rcs = [0] * k
+        ts = [threading.Thread(target=lambda i=i: rcs.__setitem__(i, call(n * i // k, n * (i + 1) // k)))
+              for i in range(k)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return next((r for r in rcs if r), 0)
     keys = device_random_bytes(n * 16, 77, dev).cpu().numpy()
     g = torch.Generator(device=dev)
     g.manual_seed(78)
@@ -913,6 +925,10 @@ def time_host_inclusive(args, dev):
                                                         hb.MEM_HOST), 3),
         ("var_pinned", lambda: lib.shf_hash_batch_var(pd.data_ptr(), poff.data_ptr(), n, SEED, vpo.data_ptr(),
                                                       hb.MEM_HOST), 3),
+        # the reference's usage model, many threads of one process (test.f.shf.c:274-336): 16 threads each
+        # hash a 1/16 slice of the same pageable batch at once, sharing the one staging pool
+        ("fixed16_pageable_x16", lambda: _threaded(16, lambda lo, hi: lib.shf_hash_batch_fixed(
+            keys.ctypes.data + lo * 16, 16, hi - lo, SEED, out.ctypes.data + lo * 16, hb.MEM_HOST)), 5),
     ]
     for name, fn, reps in cases:
         rc = fn()

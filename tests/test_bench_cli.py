@@ -213,7 +213,8 @@ def test_stdout_line_fits_the_driver_tail_at_one_and_eight_ranks():
     cpu = {"value": 1.476e8, "unit": "keys/s", "cores": 1, "kind": "reference", "sample": "x" * 400,
            "host_cpus": {"visible": 256}, "threads16": {"value": 2.1e9, "unit": "keys/s", "cores": 16, "sample": "y"}}
     hi = {"unit": "keys/s", "note": "n" * 500, "verified": True}
-    for k in ("fixed16_pageable", "fixed16_pinned", "fixed16_pinned_staged", "var_pageable", "var_pinned"):
+    for k in ("fixed16_pageable", "fixed16_pinned", "fixed16_pinned_staged", "var_pageable", "var_pinned",
+              "fixed16_pageable_x16"):
         hi[k] = {"value": 2.5e9, "value_min": 2.4e9, "value_max": 2.6e9, "repeats": 5}
     for world in (1, 8):
         full, line = _compact(world, cpu if world == 1 else None, hi if world == 1 else None)
