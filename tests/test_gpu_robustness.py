@@ -230,6 +230,45 @@ def test_concurrent_threads_share_the_staging_pool(hb, dev, oracle):
     assert torch.cuda.mem_get_info()[0] >= free0 - (8 << 20)
 
 
+def test_a_parked_context_starts_clean(hb, dev, oracle):
+    """A thread that exits leaves its per-device state parked for the next
+    thread (no HIP call at thread exit): a status a dead thread never queried
+    must not reach the thread that picks its state up, and release() frees
+    every parked context (include/shf_hash_batch.h shf_hash_batch_release)."""
+    lib = hb.load()
+    data, off, bad = _malformed(seed=9)
+    n = off.size - 1
+    d, o, out = _dev_bufs(data, off, n, dev)
+    torch.cuda.synchronize()
+    seen = {}
+
+    def dirty():  # an async call that flags a bad key, never queried; the thread exits
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        seen["dirty"] = lib.shf_hash_batch_var_async(d.data_ptr(), o.data_ptr(), n, 12345, out.data_ptr(), s)
+        torch.cuda.synchronize()
+
+    def clean():  # the next thread (likely on the parked state): nothing pending
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        seen["clean"] = lib.shf_hash_batch_status(s)
+        keys = np.frombuffer(splitmix_bytes(70_000 * 16, 91), dtype=np.uint8)
+        got = np.empty((70_000, 2), dtype=np.uint64)
+        seen["host"] = lib.shf_hash_batch_fixed(keys.ctypes.data, 16, 70_000, 12345, got.ctypes.data, hb.MEM_HOST)
+        seen["ok"] = np.array_equal(got, oracle.hash_fixed(keys, 16))
+
+    for f in (dirty, clean, clean):
+        t = threading.Thread(target=f)
+        t.start()
+        t.join()
+    assert seen["dirty"] == 0 and seen["clean"] == hb.OK and seen["host"] == 0 and seen["ok"]
+    assert lib.shf_hash_batch_release() == 0
+    # and everything starts afresh afterwards, on this thread and on a new one
+    assert lib.shf_hash_batch_status(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == hb.OK
+    t = threading.Thread(target=clean)
+    t.start()
+    t.join()
+    assert seen["clean"] == hb.OK and seen["ok"]
+
+
 @pytest.mark.parametrize("pool_mb", ["1", "32"])
 def test_threads_wait_for_slots_of_a_small_pool(hb, dev, oracle, monkeypatch, pool_mb):
     """8 threads, fixed- and variable-length host batches at once, through a
