@@ -804,3 +804,9 @@ def device_count():
 
 def check_device():
     _check(load().shf_hash_batch_check_device(), "shf_hash_batch_check_device")
+
+
+def release():
+    """shf_hash_batch_release(): free the calling thread's per-device state, the
+    state exited threads left for reuse, and the staging pools' idle slots."""
+    _check(load().shf_hash_batch_release(), "shf_hash_batch_release")
