@@ -9,7 +9,7 @@ mkdir -p $out
 rc=0
 if [ -z "$NO_TESTS" ]; then
   if [ -n "$K" ]; then kflag=(-k "$K"); else kflag=(); fi
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${kflag[@]}" \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread "${kflag[@]}" \
     > $out/pytest_gpu.log 2>&1
   rc=$?
   echo "pytest rc=$rc"
