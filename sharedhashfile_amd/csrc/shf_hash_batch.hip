@@ -384,12 +384,15 @@ bool is_host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// memcpy split over a few threads (SHF_HB_COPY_THREADS, default 8, read per
-// call): one core cannot keep up with PCIe.
+// memcpy split over a few threads (SHF_HB_COPY_THREADS, default 12, read per
+// call): one core cannot keep up with PCIe. 10M x 16-B pageable keys with
+// streaming stores, G keys/s per repeat (profiles/r5/pool_sweep/): 12 threads
+// 2.1-2.27 on both passes, 8 threads 1.5-1.9 on one and 2.35-2.4 on the other,
+// 16 threads 1.7-2.1; memcpy instead of streaming stores 1.5-1.96.
 size_t copy_threads() {
   const char* e = getenv("SHF_HB_COPY_THREADS");
   const long v = e ? strtol(e, nullptr, 10) : 0;
-  return v >= 1 && v <= 64 ? (size_t)v : 8;
+  return v >= 1 && v <= 64 ? (size_t)v : 12;
 }
 
 // Persistent staging-copy workers shared by every calling thread: started on
