@@ -2,7 +2,7 @@
 // free of HIP so that it compiles with g++ -fsanitize=address,undefined and is
 // unit-tested on the CPU (tests/c/test_host_plan.cpp, tests/test_host_plan.py):
 //
-//   * slot_layout / fixed_chunk_keys / var_chunk_end: how one chunk of keys, its
+//   * slot_layout / fixed_chunk_keys / var_chunk_end / var_chunks_estimate: how one chunk of keys, its
 //     hash records, probe records and offsets are carved out of one staging slot
 //     (a pinned host arena and a device arena of the same size);
 //   * stream_copy_avx2: the staging copies' non-temporal memcpy;
@@ -89,6 +89,16 @@ inline uint64_t var_chunk_end(const uint64_t* offsets, uint64_t i0, uint64_t n, 
       hi = mid - 1;
   }
   return lo;
+}
+
+// About how many chunks var_chunk_end cuts a batch of n keys and key_bytes bytes
+// into (at least 1): what a call asks the pool for, no more slots than it can use.
+inline uint64_t var_chunks_estimate(uint64_t key_bytes, uint64_t n, size_t slot_bytes, bool probe) {
+  const uint64_t per_key = kHashBytes + kOffBytes + (probe ? kProbeBytes : 0);
+  const uint64_t room = slot_bytes > 4 * kAlign ? slot_bytes - 4 * kAlign : 1;
+  uint64_t need = 0;
+  if (__builtin_mul_overflow(n, per_key, &need) || __builtin_add_overflow(need, key_bytes, &need)) return UINT64_MAX;
+  return std::max<uint64_t>(1, (need + room - 1) / room);
 }
 
 // memcpy with non-temporal 32-B stores (the CPU must have AVX2): head bytes up

@@ -756,10 +756,11 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     }
   }
   const bool probe = job.probe != nullptr;
-  if (!shfhb::plan::fixed_chunk_keys(std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), key_len, probe))
-    return host_fixed_big(c->dev, keys, key_len, n, seed, job);
-  Lease L;
-  if ((rc = lease_slots(c->dev, pipeline_slots(), &L))) return rc;
+  const uint64_t per = shfhb::plan::fixed_chunk_keys(std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), key_len,
+                                                     probe);
+  if (!per) return host_fixed_big(c->dev, keys, key_len, n, seed, job);
+  Lease L;  // no more slots than the batch has chunks: the rest stay free for other threads' calls
+  if ((rc = lease_slots(c->dev, (int)std::min<uint64_t>((n + per - 1) / per, pipeline_slots()), &L))) return rc;
   const uint64_t chunk = std::min<uint64_t>(shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe), n);
   const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false);
   const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
@@ -802,8 +803,10 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
   int rc = current_ctx(&c);
   if (rc) return rc;
   const bool probe = job.probe != nullptr;
-  Lease L;
-  if ((rc = lease_slots(c->dev, pipeline_slots(), &L))) return rc;
+  Lease L;  // about as many slots as the batch has chunks (host_plan.h var_chunks_estimate)
+  const uint64_t est = shfhb::plan::var_chunks_estimate(offsets[n] - offsets[0], n,
+                                                        std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), probe);
+  if ((rc = lease_slots(c->dev, (int)std::min<uint64_t>(est, pipeline_slots()), &L))) return rc;
   const size_t slot_bytes = L.s[0]->bytes;
   const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
              hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);

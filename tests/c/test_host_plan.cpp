@@ -86,6 +86,14 @@ static void walk_var(const std::vector<uint64_t>& off, size_t slot, bool probe) 
     ++chunks;
   }
   CHECK(i0 == n);
+  // the estimate a call leases slots by: never more than one below the chunks actually cut, and above
+  // them only by what keys too long for a slot add (each is cut alone, its bytes staged elsewhere)
+  const uint64_t est = var_chunks_estimate(off[n] - off[0], n, slot, probe);
+  uint64_t alone_bytes = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (slot_layout(off[i + 1] - off[i], 1, probe, true).end > slot) alone_bytes += off[i + 1] - off[i];
+  CHECK(est >= 1 && est + 1 >= chunks);
+  CHECK(est <= chunks + 1 + alone_bytes / (slot / 2));
 }
 
 static void test_var_chunks() {
