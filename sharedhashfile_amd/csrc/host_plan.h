@@ -67,6 +67,15 @@ inline uint64_t fixed_chunk_keys(size_t slot_bytes, uint32_t key_len, bool probe
   return c;
 }
 
+// Keys per chunk when n keys go in chunks of at most `most`: as few chunks as
+// that allows, of equal size (the last one never a sliver that drains the
+// pipeline alone). 0 when most is 0.
+inline uint64_t even_chunk(uint64_t n, uint64_t most) {
+  if (!most || !n) return most ? 1 : 0;
+  const uint64_t chunks = (n + most - 1) / most;
+  return (n + chunks - 1) / chunks;
+}
+
 // Variable-length keys from key i0 (offsets[i0..n] non-decreasing): the end i1 of
 // the longest chunk [i0, i1) whose key bytes, records and offsets fit one slot.
 // A single key too long for the slot gives i1 = i0 + 1 with *alone = true: its

@@ -761,7 +761,7 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   if (!per) return host_fixed_big(c->dev, keys, key_len, n, seed, job);
   Lease L;  // no more slots than the batch has chunks: the rest stay free for other threads' calls
   if ((rc = lease_slots(c->dev, (int)std::min<uint64_t>((n + per - 1) / per, pipeline_slots()), &L))) return rc;
-  const uint64_t chunk = std::min<uint64_t>(shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe), n);
+  const uint64_t chunk = shfhb::plan::even_chunk(n, shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe));
   const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false);
   const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
              probe_pinned = is_host_pinned(job.probe);

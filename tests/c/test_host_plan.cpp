@@ -59,6 +59,15 @@ static void test_fixed_chunks() {
       }
   // the default slot holds the round-4 chunk of 16-B keys (8 MiB of keys)
   CHECK(fixed_chunk_keys((size_t)16 << 20, 16, false) == ((size_t)16 << 20) / 32);
+  // even chunks: never more chunks than the slot size forces, none above it, sizes within one chunk's rounding
+  for (uint64_t most : {1ull, 7ull, 512ull << 10, 1000003ull})
+    for (uint64_t n : {1ull, 6ull, 7ull, 8ull, 625000ull, 10000000ull, 1000000007ull}) {
+      const uint64_t c = even_chunk(n, most);
+      const uint64_t chunks = (n + c - 1) / c;
+      CHECK(c >= 1 && c <= most && chunks == (n + most - 1) / most);
+      CHECK(n - (chunks - 1) * c <= c && n - (chunks - 1) * c + chunks > c);  // the last chunk is about as big
+    }
+  CHECK(even_chunk(100, 0) == 0 && even_chunk(0, 5) == 1);
   // a key at the reference's limit never fits a slot
   CHECK(fixed_chunk_keys((size_t)16 << 20, 0x7fffffffu, false) == 0);
   CHECK(fixed_chunk_keys(2 * kAlign - 1, 1, false) == 0);  // not even the key's own 256-B region and its record
