@@ -459,10 +459,7 @@ CopyPool& copy_pool() {
 // SHF_HB_COPY_NT=0 (read per call) uses memcpy throughout.
 bool copy_nt() {
   const char* e = getenv("SHF_HB_COPY_NT");
-  static const bool avx2 = [] {
-    __builtin_cpu_init();  // the CPU model may not be filled in yet when the first call comes from a constructor
-    return __builtin_cpu_supports("avx2") != 0;
-  }();
+  static const bool avx2 = __builtin_cpu_supports("avx2");  // (the runtime's constructor filled the CPU model in)
   return avx2 && !(e && e[0] == '0');
 }
 
