@@ -137,7 +137,8 @@ __attribute__((target("avx2"))) inline void stream_copy_avx2(void* dst, const vo
 // A bounded pool of staging slots, shared by every thread of the process that
 // stages host memory for one device. A call borrows between one and `want`
 // slots: the first blocks until a slot is free (or may be made), the others are
-// taken only if free right now, so no caller ever waits while holding slots and
+// taken only if free right now and no other call is waiting, so no caller ever
+// waits while holding slots, slots spread over the callers under contention, and
 // the pool cannot deadlock (as long as no caller borrows again while it holds
 // slots: the library never nests its leases). Slots are made lazily, at most max_slots of them at
 // once, and one of another size (SHF_HB_STAGE_MB changed) is remade on reuse.
@@ -165,8 +166,13 @@ class SlotPool {
         max_slots_ = max_slots;
         bytes_ = bytes;
         auto can = [&] { return !idle_.empty() || live_ < max_slots_; };
+        ++waiting_;
         cv_.wait(lk, can);
-        while (*got + to_make < want && can()) {
+        --waiting_;
+        // beyond its first slot a call takes more only while no other call waits for one: under
+        // contention the slots spread over the callers (one chunk in flight each) instead of
+        // deepening one caller's pipeline while the others queue
+        while (*got + to_make < want && can() && (*got + to_make == 0 || waiting_ == 0)) {
           if (!idle_.empty()) {
             Slot* s = idle_.back();
             idle_.pop_back();
@@ -238,6 +244,10 @@ class SlotPool {
     std::lock_guard<std::mutex> lk(mu_);
     return (int)idle_.size();
   }
+  int waiting() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return waiting_;
+  }
 
  private:
   Make make_;
@@ -246,6 +256,7 @@ class SlotPool {
   std::condition_variable cv_;
   std::vector<Slot*> idle_;
   int live_ = 0;  // slots being made, idle, on loan or being freed
+  int waiting_ = 0;  // calls waiting for their first slot
   int max_slots_ = 1;
   size_t bytes_ = 0;
 

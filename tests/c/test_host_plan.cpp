@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <random>
 #include <thread>
 #include <vector>
@@ -235,6 +236,32 @@ static void test_pool() {
   CHECK(pool.live() <= 1);
   pool.trim();
   CHECK(alive.load() == 0);
+  // while a call waits for its first slot, a returning borrower's slots go one per caller:
+  // A holds all four; B waits; A gives two back; C then gets only one (B is served first or
+  // B takes one of them and C the other), never both.
+  {
+    FakeSlot* a[4] = {};
+    int na = 0;
+    CHECK(pool.acquire(4096, 4, 4, a, &na) == 0 && na == 4);
+    std::atomic<int> nb{-1};
+    FakeSlot* b[4] = {};
+    std::thread tb([&] {
+      int k = 0;
+      CHECK(pool.acquire(4096, 4, 4, b, &k) == 0);
+      nb = k;
+    });
+    while (true) {  // until B is waiting
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      if (pool.waiting() == 1) break;
+    }
+    pool.release(a, 2);
+    tb.join();
+    CHECK(nb.load() >= 1 && nb.load() <= 2);
+    pool.release(a + 2, 2);
+    pool.release(b, nb.load());
+    pool.trim();
+    CHECK(alive.load() == 0);
+  }
   printf("pool: %d slots made, peak %d alive, %d injected failures\n", made.load(), peak.load(), errors.load());
 }
 
