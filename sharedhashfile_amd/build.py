@@ -21,7 +21,7 @@ SOURCES = ["kernels.hip", "shf_hash_batch.hip", "tab_copy.hip", "win_order.hip"]
 BENCH_CSRC = os.path.join(PKG, "csrc_bench")
 BENCH_LIB = os.path.join(PKG, "libshf_hb_bench.so")
 BENCH_SOURCES = ["hbm_ceiling.hip"]
-HEADERS = ["kernels.h", "murmur3_mix.h", "win_rank.h"]
+HEADERS = ["kernels.h", "murmur3_mix.h", "win_rank.h", "host_plan.h"]
 ARCH = "gfx950"
 
 
