@@ -89,8 +89,9 @@ constexpr uint32_t kMaxKeyLen = 0x7fffffffu;      // murmurhash3.c:75 takes `con
 // (default 16) with its own stream, and the pool holds at most SHF_HB_POOL_MB
 // MiB of them (default 64, i.e. 64 MiB of device and 64 MiB of pinned memory
 // per device, whatever the number of threads). A call borrows up to
-// SHF_HB_SLOTS (1..4, default 4) slots, one chunk in flight on each. All three
-// are read on every call. A 16-MiB slot carries 512 Ki 16-B keys with their
+// SHF_HB_SLOTS (1..4, default 4) slots, no more than its batch has chunks, and
+// beyond the first only while no other call waits; one chunk in flight on
+// each. All three are read on every call. A 16-MiB slot carries 512 Ki 16-B keys with their
 // records (the 8 MiB x 4 chunks of round 4: 10M x 16 B pageable 2.04, page-
 // locked staged 2.19 G keys/s; profiles/r4/stage_sweep/), or ~15 MiB of
 // variable-length keys with their offsets and records.
