@@ -330,6 +330,43 @@ def test_threads_wait_for_slots_of_a_small_pool(hb, dev, oracle, monkeypatch, po
     assert ok == [True] * 8
 
 
+def test_processes_hash_at_once(hb, dev, oracle, tmp_path):
+    """The reference's multi-process model (test.f.shf.c:274-336: children that
+    each put their own key range): four processes, each with its own staging
+    pool and contexts, hash their ranges of one batch through the host and the
+    device paths at the same time; every result bit-exact."""
+    import subprocess
+    import sys
+
+    n, procs = 400_000, 4
+    keys = np.frombuffer(splitmix_bytes(n * 16, 95), dtype=np.uint8).copy()
+    src = tmp_path / "keys.bin"
+    keys.tofile(src)
+    child = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[4])
+import sharedhashfile_amd as hb
+lo, hi = int(sys.argv[2]), int(sys.argv[3])
+keys = np.fromfile(sys.argv[1], dtype=np.uint8)[lo * 16:hi * 16].copy()
+out = np.empty((hi - lo, 2), dtype=np.uint64)
+assert hb.load().shf_hash_batch_fixed(keys.ctypes.data, 16, hi - lo, 12345, out.ctypes.data, hb.MEM_HOST) == 0
+d = hb.hash_fixed(torch.from_numpy(keys).to("cuda:0"), 16)
+torch.cuda.synchronize()
+assert np.array_equal(d.cpu().numpy().view(np.uint64), out)
+out.tofile(sys.argv[1] + ".%d" % lo)
+"""
+    root = str(__import__("pathlib").Path(__file__).resolve().parents[1])
+    ps = [subprocess.Popen([sys.executable, "-c", child, str(src), str(n * i // procs), str(n * (i + 1) // procs), root],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for i in range(procs)]
+    for p in ps:
+        _, err = p.communicate(timeout=180)
+        assert p.returncode == 0, err[-2000:]
+    want = oracle.hash_fixed(keys, 16, threads=8)
+    got = np.concatenate([np.fromfile(str(src) + ".%d" % (n * i // procs), dtype=np.uint64).reshape(-1, 2)
+                          for i in range(procs)])
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("n_devices", [2, 3])
 def test_multi_split_with_shared_device(hb, dev, oracle, monkeypatch, n_devices):
     """shf_hash_batch_*_multi's split (one host thread per shard, contiguous key
