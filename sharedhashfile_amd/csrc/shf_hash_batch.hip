@@ -19,6 +19,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -399,8 +400,43 @@ size_t copy_threads() {
 // Persistent staging-copy workers shared by every calling thread: started on
 // first use (up to SHF_HB_COPY_THREADS - 1), never per chunk. Deliberately
 // never destroyed: the workers park on the queue and end with the process.
+// A batch of pieces handed to the pool's workers: wait() returns once every
+// piece has run, with the first non-zero status a piece returned.
+struct Ticket {
+  std::mutex m;
+  std::condition_variable cv;
+  size_t left = 0;
+  int rc = 0;
+  void done(int r) {
+    std::lock_guard<std::mutex> lk(m);
+    if (r && !rc) rc = r;
+    if (--left == 0) cv.notify_all();
+  }
+  int wait() {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return left == 0; });
+    return rc;
+  }
+};
+
 class CopyPool {
  public:
+  // Runs every piece on the workers and returns at once (Ticket::wait() joins them).
+  std::shared_ptr<Ticket> submit(std::vector<std::function<int()>> pieces) {
+    auto t = std::make_shared<Ticket>();
+    t->left = pieces.size();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (workers_ < pieces.size()) {
+        std::thread([this] { work(); }).detach();
+        ++workers_;
+      }
+      for (auto& f : pieces) q_.push_back([t, f] { t->done(f()); });
+    }
+    cv_.notify_all();
+    return t;
+  }
+
   void run(const std::vector<std::function<void()>>& pieces) {  // pieces[0] runs on the caller
     struct Latch {
       std::mutex m;
@@ -507,6 +543,10 @@ struct Pending {
   shf_probe* probe = nullptr;
   const shf_probe* probe_src = nullptr;
   uint64_t count = 0;
+  std::shared_ptr<struct Ticket> copy_out;  // the copy-out running on the copy workers (drain_async)
+  ~Pending() {
+    if (copy_out) (void)copy_out->wait();  // on every path: the slot goes back to the pool only after it
+  }
 };
 
 // SHF_HB_TRACE=1 (read once): each host-pipeline call prints one line on
@@ -533,6 +573,12 @@ double now_ms() {
 
 int drain_slot(Slot* s, Pending& p) {
   if (!p.busy) return SHF_HB_OK;
+  if (p.copy_out) {  // handed to the workers by drain_async: wait for them
+    const int rc = p.copy_out->wait();
+    p.copy_out.reset();
+    p.busy = false;
+    return rc;
+  }
   const bool tr = trace_on();
   const double t0 = tr ? now_ms() : 0;
   HB_TRY(hipEventSynchronize(s->done));
@@ -545,6 +591,33 @@ int drain_slot(Slot* s, Pending& p) {
   }
   p.busy = false;
   return SHF_HB_OK;
+}
+
+// drain_slot's work handed to the copy workers, the caller going on at once: each
+// piece waits for the slot's event, then copies its part of the records out.
+// Used where the caller spends the chunk's time inside a blocking copy of its
+// own (the runtime's pageable H2D), so the copy-out runs beside it.
+void drain_async(Slot* s, Pending& p) {
+  if (!p.busy || p.copy_out || (!p.hash && !p.probe)) return;
+  constexpr size_t kMinPiece = (size_t)2 << 20;
+  std::vector<std::function<int()>> pieces;
+  const bool nt = copy_nt();
+  auto split = [&](void* dst, const void* src, size_t n) {
+    const size_t k = std::min<size_t>(copy_threads(), std::max<size_t>(1, n / kMinPiece)), per = (n + k - 1) / k;
+    for (size_t a = 0; a < n; a += per) {
+      const size_t b = std::min(n, a + per);
+      hipEvent_t ev = s->done;
+      pieces.emplace_back([=] {
+        const hipError_t e = hipEventSynchronize(ev);
+        if (e != hipSuccess) return map_hip(e);
+        copy_piece((char*)dst + a, (const char*)src + a, b - a, nt);
+        return (int)SHF_HB_OK;
+      });
+    }
+  };
+  if (p.hash) split(p.hash, p.hash_src, p.count * sizeof(shf_hash128));
+  if (p.probe) split(p.probe, p.probe_src, p.count * sizeof(shf_probe));
+  p.copy_out = copy_pool().submit(std::move(pieces));
 }
 
 int drain_all(Lease& L, Pending* pend) {
@@ -739,6 +812,19 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
 // pageable-copy path; a library must not put its caller's unrelated copies at
 // risk for 15 %, so the path is gone.
 
+// Pageable keys (and offsets) go to the device through the HIP runtime's own
+// pageable copy (hipMemcpyAsync from the caller's memory, which holds the
+// calling thread until its bytes are on their way), while the copy workers
+// move each earlier chunk's records out (drain_async); SHF_HB_RUNTIME_H2D=0
+// copies them into the slot's pinned arena on the CPU first instead. The
+// runtime moves pageable bytes at 49-56 GB/s, as fast as page-locked ones,
+// and two threads' pageable copies in opposite directions overlap (81 GB/s
+// together at 8-MiB chunks; tools/pageable_*_probe.py, profiles/r5/runtime_copy/).
+bool runtime_h2d() {
+  const char* e = getenv("SHF_HB_RUNTIME_H2D");
+  return !(e && e[0] == '0');
+}
+
 // Host-memory fixed-length pipeline on the current device.
 int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t seed, const HostJob& job_in) {
   const HostJob job = with_direct_out(job_in, n);
@@ -766,6 +852,7 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false);
   const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
              probe_pinned = is_host_pinned(job.probe);
+  const bool via_runtime = !in_pinned && runtime_h2d();
   if (trace_on()) tls_trace.slots = L.n;
   Pending pend[kMaxSlots];
   uint64_t idx = 0;
@@ -776,16 +863,17 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
     const ChunkBufs b = carve(s, lay);
     const uint64_t cnt = std::min(chunk, n - i0);
     const size_t nb = (size_t)cnt * key_len;
-    const uint8_t* src = in_pinned ? keys + i0 * key_len : b.h_in;
+    const uint8_t* src = (in_pinned || via_runtime) ? keys + i0 * key_len : b.h_in;
     const double t0 = trace_on() ? now_ms() : 0;
-    if (nb && !in_pinned) par_memcpy(b.h_in, keys + i0 * key_len, nb);
-    const double t1 = trace_on() ? now_ms() : 0;
+    if (nb && !in_pinned && !via_runtime) par_memcpy(b.h_in, keys + i0 * key_len, nb);
     if (nb) HB_TRY(hipMemcpyAsync(b.d_in, src, nb, hipMemcpyHostToDevice, s->st));
+    const double t1 = trace_on() ? now_ms() : 0;
     shfhb::Sink k;
     int mode = 0;
     job_sink(b, job, i0, &k, &mode);
     HB_TRY(shfhb::launch_fixed(b.d_in, key_len, cnt, seed, k, mode, s->st, shfhb::kKernelAuto));
     if ((rc = job_d2h(s, b, job, i0, cnt, hash_pinned, probe_pinned, &pend[q]))) return rc;
+    if (via_runtime) drain_async(s, pend[q]);
     if (trace_on()) {
       tls_trace.copy_in += t1 - t0;
       tls_trace.enqueue += now_ms() - t1;
@@ -811,6 +899,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
   const size_t slot_bytes = L.s[0]->bytes;
   const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
              hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
+  const bool via_runtime = !(in_pinned && off_pinned) && runtime_h2d();
   Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
@@ -830,14 +919,15 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     }
     const ChunkBufs b = carve(s, shfhb::plan::slot_layout(alone ? 0 : nb, cnt, probe, true));
     uint8_t* d_in = alone ? (uint8_t*)tmp.p : b.d_in;
-    if (nb && !in_pinned && !alone) par_memcpy(b.h_in, bytes + base, nb);
+    if (nb && !in_pinned && !alone && !via_runtime) par_memcpy(b.h_in, bytes + base, nb);
     const uint64_t* off_src = offsets + i0;
-    if (!off_pinned) {
+    if (!off_pinned && !via_runtime) {
       par_memcpy(b.h_off, offsets + i0, (cnt + 1) * sizeof(uint64_t));
       off_src = b.h_off;
     }
     if (nb)
-      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || alone) ? bytes + base : b.h_in, nb, hipMemcpyHostToDevice, s->st));
+      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || alone || via_runtime) ? bytes + base : b.h_in, nb,
+                            hipMemcpyHostToDevice, s->st));
     HB_TRY(hipMemcpyAsync(b.d_off, off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s->st));
     shfhb::Sink k;
     int mode = 0;
@@ -846,6 +936,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     HB_TRY(shfhb::launch_var(d_in, b.d_off, base, cnt, seed, k, mode, s->st, shfhb::kKernelAuto, nb));
     if ((rc = job_d2h(s, b, job, i0, cnt, hash_pinned, probe_pinned, &pend[q]))) return rc;
     if (alone && (rc = drain_slot(s, pend[q]))) return rc;  // before tmp is freed
+    if (via_runtime) drain_async(s, pend[q]);
     i0 = i1;
   }
   return drain_all(L, pend);
