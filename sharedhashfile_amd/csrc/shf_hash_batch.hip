@@ -812,7 +812,7 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
 // pageable-copy path; a library must not put its caller's unrelated copies at
 // risk for 15 %, so the path is gone.
 
-// Pageable keys (and offsets) go to the device through the HIP runtime's own
+// Pageable fixed-length keys go to the device through the HIP runtime's own
 // pageable copy (hipMemcpyAsync from the caller's memory, which holds the
 // calling thread until its bytes are on their way), while the copy workers
 // move each earlier chunk's records out (drain_async); SHF_HB_RUNTIME_H2D=0
@@ -820,6 +820,8 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
 // runtime moves pageable bytes at 49-56 GB/s, as fast as page-locked ones,
 // and two threads' pageable copies in opposite directions overlap (81 GB/s
 // together at 8-MiB chunks; tools/pageable_*_probe.py, profiles/r5/runtime_copy/).
+// 10M x 16-B pageable keys: 2.34-2.39 against 1.96-2.17 G keys/s staged on
+// the CPU, 16 threads at once 2.18-2.27 against 1.89-1.95 (same box, alternating).
 bool runtime_h2d() {
   const char* e = getenv("SHF_HB_RUNTIME_H2D");
   return !(e && e[0] == '0');
@@ -899,7 +901,9 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
   const size_t slot_bytes = L.s[0]->bytes;
   const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
              hash_pinned = is_host_pinned(job.hash), probe_pinned = is_host_pinned(job.probe);
-  const bool via_runtime = !(in_pinned && off_pinned) && runtime_h2d();
+  // (staged on the CPU, not through the runtime's pageable copy: a slot's ~15 MiB of variable-
+  // length key bytes per chunk came out 7 % slower that way, 0.178-0.179 against 0.191-0.193 G
+  // keys/s on U[8,512] B; the runtime's opposite-direction copies stop overlapping at 16-32 MiB)
   Pending pend[kMaxSlots];
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
@@ -919,15 +923,14 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     }
     const ChunkBufs b = carve(s, shfhb::plan::slot_layout(alone ? 0 : nb, cnt, probe, true));
     uint8_t* d_in = alone ? (uint8_t*)tmp.p : b.d_in;
-    if (nb && !in_pinned && !alone && !via_runtime) par_memcpy(b.h_in, bytes + base, nb);
+    if (nb && !in_pinned && !alone) par_memcpy(b.h_in, bytes + base, nb);
     const uint64_t* off_src = offsets + i0;
-    if (!off_pinned && !via_runtime) {
+    if (!off_pinned) {
       par_memcpy(b.h_off, offsets + i0, (cnt + 1) * sizeof(uint64_t));
       off_src = b.h_off;
     }
     if (nb)
-      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || alone || via_runtime) ? bytes + base : b.h_in, nb,
-                            hipMemcpyHostToDevice, s->st));
+      HB_TRY(hipMemcpyAsync(d_in, (in_pinned || alone) ? bytes + base : b.h_in, nb, hipMemcpyHostToDevice, s->st));
     HB_TRY(hipMemcpyAsync(b.d_off, off_src, (cnt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s->st));
     shfhb::Sink k;
     int mode = 0;
@@ -936,7 +939,6 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     HB_TRY(shfhb::launch_var(d_in, b.d_off, base, cnt, seed, k, mode, s->st, shfhb::kKernelAuto, nb));
     if ((rc = job_d2h(s, b, job, i0, cnt, hash_pinned, probe_pinned, &pend[q]))) return rc;
     if (alone && (rc = drain_slot(s, pend[q]))) return rc;  // before tmp is freed
-    if (via_runtime) drain_async(s, pend[q]);
     i0 = i1;
   }
   return drain_all(L, pend);
