@@ -574,7 +574,9 @@ double now_ms() {
 int drain_slot(Slot* s, Pending& p) {
   if (!p.busy) return SHF_HB_OK;
   if (p.copy_out) {  // handed to the workers by drain_async: wait for them
+    const double t0 = trace_on() ? now_ms() : 0;
     const int rc = p.copy_out->wait();
+    if (trace_on()) tls_trace.wait += now_ms() - t0;
     p.copy_out.reset();
     p.busy = false;
     return rc;
@@ -597,13 +599,18 @@ int drain_slot(Slot* s, Pending& p) {
 // piece waits for the slot's event, then copies its part of the records out.
 // Used where the caller spends the chunk's time inside a blocking copy of its
 // own (the runtime's pageable H2D), so the copy-out runs beside it.
+// At most four pieces per copy-out: beside the runtime's pageable H2D, 4-6 copy threads
+// gave 2.39-2.40 G keys/s on 10M x 16-B keys in both rounds of an alternating sweep, 8-16
+// threads 2.24-2.40 and 2 threads 2.18-2.38 (more threads take host memory bandwidth from
+// the runtime's own copy; profiles/r5/runtime_copy/threads_sweep.txt).
 void drain_async(Slot* s, Pending& p) {
   if (!p.busy || p.copy_out || (!p.hash && !p.probe)) return;
-  constexpr size_t kMinPiece = (size_t)2 << 20;
+  constexpr size_t kMinPiece = (size_t)2 << 20, kMaxPieces = 4;
   std::vector<std::function<int()>> pieces;
   const bool nt = copy_nt();
   auto split = [&](void* dst, const void* src, size_t n) {
-    const size_t k = std::min<size_t>(copy_threads(), std::max<size_t>(1, n / kMinPiece)), per = (n + k - 1) / k;
+    const size_t k = std::min<size_t>({copy_threads(), kMaxPieces, std::max<size_t>(1, n / kMinPiece)}),
+                 per = (n + k - 1) / k;
     for (size_t a = 0; a < n; a += per) {
       const size_t b = std::min(n, a + per);
       hipEvent_t ev = s->done;

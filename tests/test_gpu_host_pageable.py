@@ -85,3 +85,42 @@ def test_reused_addresses_copy_cleanly(hb, dev, oracle):
         back = t.cpu().numpy()
         torch.cuda.synchronize()
         assert np.array_equal(back, fresh)
+
+
+@pytest.mark.parametrize("runtime_h2d,copy_nt,threads,direct_out",
+                         [("1", "1", "12", "1"), ("0", "1", "12", "1"), ("1", "0", "1", "1"), ("0", "0", "3", "0"),
+                          ("1", "1", "2", "0")])
+def test_host_pageable_copy_settings(hb, dev, oracle, monkeypatch, runtime_h2d, copy_nt, threads, direct_out):
+    """Every way a pageable batch moves (read per call): keys through the
+    runtime's pageable copy with the records copied out on the copy workers
+    (SHF_HB_RUNTIME_H2D=1) or staged on the CPU (0), streaming stores or
+    memcpy, 1-12 copy threads, records stored by the kernel into the slot or
+    copied back. 1-MiB slots, three of them, so every chunk's copy-out runs
+    beside a later chunk's copy-in; hashes, probe records and both at once,
+    fixed (16 B: k_fixed16; 40 B: another kernel) and variable lengths."""
+    from sharedhashfile_amd.keygen import splitmix_lengths
+    from sharedhashfile_amd.rowindex import synthetic_index
+
+    for k, v in (("SHF_HB_RUNTIME_H2D", runtime_h2d), ("SHF_HB_COPY_NT", copy_nt), ("SHF_HB_COPY_THREADS", threads),
+                 ("SHF_HB_DIRECT_OUT", direct_out), ("SHF_HB_STAGE_MB", "1"), ("SHF_HB_SLOTS", "3")):
+        monkeypatch.setenv(k, v)
+    for key_len, n in ((16, 400_003), (40, 150_001)):
+        flat = np.frombuffer(splitmix_bytes(n * key_len, 70 + key_len), dtype=np.uint8)
+        want = oracle.hash_fixed(flat, key_len, threads=8)
+        assert np.array_equal(hb.hash_fixed_host(flat, key_len), want)
+    m = 60_000
+    off = np.zeros(m + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(splitmix_lengths(m, 8, 512, 73))
+    data = np.frombuffer(splitmix_bytes(int(off[-1]), 74), dtype=np.uint8)
+    assert np.array_equal(hb.hash_var_host(data, off), oracle.hash_var(data, off))
+    keys = np.frombuffer(splitmix_bytes(300_007 * 16, 75), dtype=np.uint8).reshape(-1, 16)
+    h = oracle.hash_fixed(keys.reshape(-1), 16, threads=8)
+    tab_slot, rows, n_slots, _ = synthetic_index(h, tabs_per_win=2, limit=len(h) - 1000)
+    idx = hb.RowIndex(n_slots, tab_slot, rows)
+    try:
+        want = oracle.probe(h, tab_slot, rows)
+        rec, hh = hb.probe_fixed_host(idx, keys, hashes=True)
+        assert np.array_equal(rec, want) and np.array_equal(hh, h)
+        assert np.array_equal(hb.probe_fixed_host(idx, keys), want)
+    finally:
+        idx.close()
