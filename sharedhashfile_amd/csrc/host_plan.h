@@ -7,7 +7,9 @@
 //     (a pinned host arena and a device arena of the same size);
 //   * stream_copy_avx2: the staging copies' non-temporal memcpy;
 //   * SlotPool: the per-device pool of staging slots that every calling thread
-//     borrows from (a bounded footprint per process, not per thread).
+//     borrows from (a bounded footprint per process, not per thread);
+//   * CopyPool / Ticket: the staging copies' worker threads, with batches run
+//     in place (run) or handed off and joined later (submit, Ticket::wait).
 //
 // Key lengths follow the reference's contract: MurmurHash3_x64_128 takes
 // `const int len` (/root/reference/src/murmurhash3.c:75), so a key is < 2^31 B;
@@ -21,8 +23,11 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace shfhb {
@@ -271,6 +276,101 @@ class SlotPool {
     cv_.notify_all();
     v.clear();
   }
+};
+
+// A batch of pieces handed to a CopyPool's workers: wait() returns once every
+// piece has run, with the first non-zero status a piece returned.
+struct Ticket {
+  std::mutex m;
+  std::condition_variable cv;
+  size_t left = 0;
+  int rc = 0;
+  void done(int r) {
+    std::lock_guard<std::mutex> lk(m);
+    if (r && !rc) rc = r;
+    if (--left == 0) cv.notify_all();
+  }
+  int wait() {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return left == 0; });
+    return rc;
+  }
+};
+
+// Worker threads for the staging copies, shared by every calling thread: a
+// worker is started when a batch has more pieces than there are workers, and
+// parks on the queue between batches (the library keeps one pool for the
+// process's life). submit() returns at once with a Ticket; run() runs
+// pieces[0] on the caller and returns when every piece has run.
+class CopyPool {
+ public:
+  std::shared_ptr<Ticket> submit(std::vector<std::function<int()>> pieces) {
+    auto t = std::make_shared<Ticket>();
+    t->left = pieces.size();
+    if (pieces.empty()) return t;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      grow(pieces.size());
+      for (auto& f : pieces) q_.push_back([t, f] { t->done(f()); });
+    }
+    cv_.notify_all();
+    return t;
+  }
+
+  void run(const std::vector<std::function<void()>>& pieces) {
+    if (pieces.empty()) return;
+    struct Latch {
+      std::mutex m;
+      std::condition_variable cv;
+      size_t left;
+    } latch;
+    latch.left = pieces.size() - 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      grow(pieces.size() - 1);
+      for (size_t i = 1; i < pieces.size(); ++i) {
+        const std::function<void()>* f = &pieces[i];
+        q_.push_back([f, &latch] {
+          (*f)();
+          std::lock_guard<std::mutex> l2(latch.m);
+          if (--latch.left == 0) latch.cv.notify_one();
+        });
+      }
+    }
+    cv_.notify_all();
+    pieces[0]();
+    std::unique_lock<std::mutex> lk(latch.m);
+    latch.cv.wait(lk, [&] { return latch.left == 0; });
+  }
+
+  size_t workers() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return workers_;
+  }
+
+ private:
+  void grow(size_t want) {  // under mu_
+    while (workers_ < want) {
+      std::thread([this] { work(); }).detach();
+      ++workers_;
+    }
+  }
+  void work() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  size_t workers_ = 0;
 };
 
 }  // namespace plan

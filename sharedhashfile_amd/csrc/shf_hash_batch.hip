@@ -397,92 +397,12 @@ size_t copy_threads() {
   return v >= 1 && v <= 64 ? (size_t)v : 12;
 }
 
-// Persistent staging-copy workers shared by every calling thread: started on
-// first use (up to SHF_HB_COPY_THREADS - 1), never per chunk. Deliberately
-// never destroyed: the workers park on the queue and end with the process.
-// A batch of pieces handed to the pool's workers: wait() returns once every
-// piece has run, with the first non-zero status a piece returned.
-struct Ticket {
-  std::mutex m;
-  std::condition_variable cv;
-  size_t left = 0;
-  int rc = 0;
-  void done(int r) {
-    std::lock_guard<std::mutex> lk(m);
-    if (r && !rc) rc = r;
-    if (--left == 0) cv.notify_all();
-  }
-  int wait() {
-    std::unique_lock<std::mutex> lk(m);
-    cv.wait(lk, [&] { return left == 0; });
-    return rc;
-  }
-};
-
-class CopyPool {
- public:
-  // Runs every piece on the workers and returns at once (Ticket::wait() joins them).
-  std::shared_ptr<Ticket> submit(std::vector<std::function<int()>> pieces) {
-    auto t = std::make_shared<Ticket>();
-    t->left = pieces.size();
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      while (workers_ < pieces.size()) {
-        std::thread([this] { work(); }).detach();
-        ++workers_;
-      }
-      for (auto& f : pieces) q_.push_back([t, f] { t->done(f()); });
-    }
-    cv_.notify_all();
-    return t;
-  }
-
-  void run(const std::vector<std::function<void()>>& pieces) {  // pieces[0] runs on the caller
-    struct Latch {
-      std::mutex m;
-      std::condition_variable cv;
-      size_t left;
-    } latch;
-    latch.left = pieces.size() - 1;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      while (workers_ < pieces.size() - 1) {
-        std::thread([this] { work(); }).detach();
-        ++workers_;
-      }
-      for (size_t i = 1; i < pieces.size(); ++i) {
-        const std::function<void()>* f = &pieces[i];
-        q_.push_back([f, &latch] {
-          (*f)();
-          std::lock_guard<std::mutex> l2(latch.m);
-          if (--latch.left == 0) latch.cv.notify_one();
-        });
-      }
-    }
-    cv_.notify_all();
-    pieces[0]();
-    std::unique_lock<std::mutex> lk(latch.m);
-    latch.cv.wait(lk, [&] { return latch.left == 0; });
-  }
-
- private:
-  void work() {
-    for (;;) {
-      std::function<void()> f;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return !q_.empty(); });
-        f = std::move(q_.front());
-        q_.pop_front();
-      }
-      f();
-    }
-  }
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<std::function<void()>> q_;
-  size_t workers_ = 0;
-};
+// Persistent staging-copy workers shared by every calling thread (host_plan.h
+// CopyPool): started on first use (up to SHF_HB_COPY_THREADS - 1), never per
+// chunk. Deliberately never destroyed: the workers park on the queue and end
+// with the process.
+using shfhb::plan::CopyPool;
+using shfhb::plan::Ticket;
 
 CopyPool& copy_pool() {
   static CopyPool* p = new CopyPool();
@@ -543,7 +463,7 @@ struct Pending {
   shf_probe* probe = nullptr;
   const shf_probe* probe_src = nullptr;
   uint64_t count = 0;
-  std::shared_ptr<struct Ticket> copy_out;  // the copy-out running on the copy workers (drain_async)
+  std::shared_ptr<Ticket> copy_out;  // the copy-out running on the copy workers (drain_async)
   ~Pending() {
     if (copy_out) (void)copy_out->wait();  // on every path: the slot goes back to the pool only after it
   }

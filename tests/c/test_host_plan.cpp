@@ -265,11 +265,69 @@ static void test_pool() {
   printf("pool: %d slots made, peak %d alive, %d injected failures\n", made.load(), peak.load(), errors.load());
 }
 
+// The copy workers under 16 calling threads at once, as the library uses them:
+// run() (a staging copy split over the workers, the caller doing piece 0) mixed
+// with submit() (a copy-out handed off, joined later through its Ticket, the
+// first failing piece's status kept); every piece runs exactly once, and a
+// Ticket outlives the caller's own wait (the library's Pending waits in its
+// destructor). ThreadSanitizer checks the queue and the latches.
+static void test_copy_pool() {
+  static CopyPool* pool = new CopyPool();  // never destroyed, as in the library
+  std::vector<std::thread> ts;
+  std::atomic<int> bad{0};
+  for (int t = 0; t < 16; ++t)
+    ts.emplace_back([&, t] {
+      std::mt19937 rng(100 + t);
+      std::vector<std::shared_ptr<Ticket>> held;
+      for (int it = 0; it < 300; ++it) {
+        const size_t k = 1 + rng() % 12;
+        std::vector<int> hits(k, 0);
+        if (it % 3 == 0) {
+          std::vector<std::function<void()>> pieces;
+          for (size_t i = 0; i < k; ++i) pieces.emplace_back([&hits, i] { ++hits[i]; });
+          pool->run(pieces);
+          for (size_t i = 0; i < k; ++i)
+            if (hits[i] != 1) ++bad;
+        } else {
+          auto out = std::make_shared<std::vector<int>>(k, 0);
+          const int fail_at = (it % 7 == 0) ? (int)(rng() % k) : -1;
+          std::vector<std::function<int()>> pieces;
+          for (size_t i = 0; i < k; ++i)
+            pieces.emplace_back([out, i, fail_at] {
+              ++(*out)[i];
+              return (int)i == fail_at ? -3 : 0;
+            });
+          auto tk = pool->submit(std::move(pieces));
+          if (it % 2) {  // joined now
+            const int rc = tk->wait();
+            if (rc != (fail_at >= 0 ? -3 : 0)) ++bad;
+            for (size_t i = 0; i < k; ++i)
+              if ((*out)[i] != 1) ++bad;
+          } else {
+            held.push_back(tk);  // joined later, after more batches went through
+          }
+        }
+      }
+      for (auto& tk : held) {
+        const int rc = tk->wait();
+        if (rc != 0 && rc != -3) ++bad;
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(bad.load() == 0);
+  CHECK(pool->workers() <= 12);  // never more workers than the largest batch asked for
+  auto empty = pool->submit({});
+  CHECK(empty->wait() == 0);
+  pool->run({});
+  printf("copy pool: %zu workers, 16 threads x 300 batches\n", pool->workers());
+}
+
 int main() {
   test_fixed_chunks();
   test_var_chunks();
   test_stream_copy();
   test_pool();
+  test_copy_pool();
   if (failures) {
     fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;
