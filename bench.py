@@ -859,8 +859,10 @@ def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP
 def time_host_inclusive(args, dev):
     """Host buffers in and out (SHF_HASH_MEM_HOST): H2D keys (+ offsets) +
     kernel + D2H hashes, pipelined in SHF_HB_STAGE_MB chunks, SHF_HB_SLOTS in
-    flight. Pageable buffers are staged through pinned memory; page-locked
-    ones are DMA'd directly. Fixed 16-B keys and config-D's U[8,512] B
+    flight. Pageable fixed-length keys go through the HIP runtime's pageable
+    copy with the records copied out on the library's copy threads beside it,
+    pageable variable-length keys are staged through pinned memory on the CPU;
+    page-locked buffers are DMA'd directly. Fixed 16-B keys and config-D's U[8,512] B
     variable-length keys, --host-keys of each."""
     import torch
 
@@ -873,8 +875,9 @@ def time_host_inclusive(args, dev):
                                      "timed repeats after one untimed call; *_pinned = page-locked caller buffers "
                                      "(16-B keys: the kernel reads and writes them over PCIe, zero copy), "
                                      "*_pinned_staged = the same through hipMemcpyAsync both ways; "
-                                     "*_pageable = pageable buffers through the staged pipeline (the library never "
-                                     "page-locks a caller's pageable memory); *_x16 = 16 threads, one slice each, "
+                                     "*_pageable = pageable buffers through the pipeline (fixed-length keys by the "
+                                     "runtime's pageable copy, variable-length ones staged on the CPU; the library "
+                                     "never page-locks a caller's pageable memory); *_x16 = 16 threads, one slice each, "
                                      "at once (one staging pool)"
                                      % n}
 
