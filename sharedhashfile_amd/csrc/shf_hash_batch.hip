@@ -749,6 +749,9 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
 // together at 8-MiB chunks; tools/pageable_*_probe.py, profiles/r5/runtime_copy/).
 // 10M x 16-B pageable keys: 2.34-2.39 against 1.96-2.17 G keys/s staged on
 // the CPU, 16 threads at once 2.18-2.27 against 1.89-1.95 (same box, alternating).
+// (The records back by the runtime's pageable D2H too, issued from a copy worker beside
+// the next chunk's H2D, instead of kernel stores into the slot plus a host copy: 1.68-2.00
+// against 2.14-2.29 G keys/s, profiles/r5/runtime_copy/ab_runtime_d2h/; not kept.)
 bool runtime_h2d() {
   const char* e = getenv("SHF_HB_RUNTIME_H2D");
   return !(e && e[0] == '0');
