@@ -464,8 +464,22 @@ struct Pending {
   const shf_probe* probe_src = nullptr;
   uint64_t count = 0;
   std::shared_ptr<Ticket> copy_out;  // the copy-out running on the copy workers (drain_async)
+  Pending() = default;
+  Pending(const Pending&) = delete;
+  Pending& operator=(const Pending&) = delete;
   ~Pending() {
     if (copy_out) (void)copy_out->wait();  // on every path: the slot goes back to the pool only after it
+  }
+  // For the slot's next chunk (drain_slot has run: a copy-out still going is waited for, never dropped).
+  void reset() {
+    if (copy_out) (void)copy_out->wait();
+    busy = false;
+    hash = nullptr;
+    hash_src = nullptr;
+    probe = nullptr;
+    probe_src = nullptr;
+    count = 0;
+    copy_out.reset();
   }
 };
 
@@ -613,7 +627,7 @@ int direct_sink(const HostJob& job, void* d_out, shfhb::Sink* k) {
 // caller memory, else into the slot's pinned arena for drain_slot to copy).
 int job_d2h(Slot* s, const ChunkBufs& b, const HostJob& job, uint64_t i0, uint64_t cnt, bool hash_pinned,
             bool probe_pinned, Pending* p) {
-  *p = Pending();
+  p->reset();
   p->busy = true;
   p->count = cnt;
   if (job.hash && !job.hash_dev && job.stage_direct && !job.probe && b.hd_out) {
