@@ -28,11 +28,13 @@ def u64(t):
 
 
 def d_u8(a, dev):
-    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8).reshape(-1)).to(dev)
+    a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1)
+    return torch.from_numpy(a if a.flags.writeable else a.copy()).to(dev)
 
 
 def d_off(off, dev):
-    return torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(dev)
+    off = np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)
+    return torch.from_numpy(off if off.flags.writeable else off.copy()).to(dev)
 
 
 def fixed_kernels(key_len, aligned=True):
