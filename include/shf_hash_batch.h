@@ -78,7 +78,7 @@ extern "C" {
 
 /* Where the caller's buffers live. */
 #define SHF_HASH_MEM_DEVICE 0 /* keys, offsets and out are device (HBM) pointers */
-#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); staged through the process's pinned slots, or read and written by the kernel in place (fixed-length keys in page-locked caller buffers; pageable memory is never page-locked by the library) */
+#define SHF_HASH_MEM_HOST 1   /* host pointers (pageable or pinned); pipelined through the process's staging slots (pageable fixed-length keys by the HIP runtime's own pageable copy), or read and written by the kernel in place (fixed-length keys in page-locked caller buffers); pageable memory is never page-locked by the library */
 
 /* One result record: identical bytes to SHF_HASH (shf.private.h:180-185). */
 typedef struct shf_hash128 {
