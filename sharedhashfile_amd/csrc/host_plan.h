@@ -304,15 +304,20 @@ struct Ticket {
 // pieces[0] on the caller and returns when every piece has run.
 class CopyPool {
  public:
+  explicit CopyPool(size_t max_workers = (size_t)-1) : max_workers_(max_workers) {}
+
   std::shared_ptr<Ticket> submit(std::vector<std::function<int()>> pieces) {
     auto t = std::make_shared<Ticket>();
     t->left = pieces.size();
     if (pieces.empty()) return t;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      grow(pieces.size());
-      for (auto& f : pieces) q_.push_back([t, f] { t->done(f()); });
+      if (grow(pieces.size())) {
+        for (auto& f : pieces) q_.push_back([t, f] { t->done(f()); });
+        pieces.clear();
+      }
     }
+    for (auto& f : pieces) t->done(f());  // no worker could be started: on the caller, now
     cv_.notify_all();
     return t;
   }
@@ -325,10 +330,11 @@ class CopyPool {
       size_t left;
     } latch;
     latch.left = pieces.size() - 1;
+    bool alone = false;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      grow(pieces.size() - 1);
-      for (size_t i = 1; i < pieces.size(); ++i) {
+      alone = pieces.size() > 1 && !grow(pieces.size() - 1);  // no worker could be started
+      for (size_t i = 1; i < pieces.size() && !alone; ++i) {
         const std::function<void()>* f = &pieces[i];
         q_.push_back([f, &latch] {
           (*f)();
@@ -336,6 +342,10 @@ class CopyPool {
           if (--latch.left == 0) latch.cv.notify_one();
         });
       }
+    }
+    if (alone) {  // every piece on the caller
+      for (auto& f : pieces) f();
+      return;
     }
     cv_.notify_all();
     pieces[0]();
@@ -349,11 +359,18 @@ class CopyPool {
   }
 
  private:
-  void grow(size_t want) {  // under mu_
-    while (workers_ < want) {
-      std::thread([this] { work(); }).detach();
+  // Under mu_: starts workers up to `want`; returns how many there are (a thread the
+  // system refuses is left out, and what is queued runs on those that exist).
+  size_t grow(size_t want) {
+    while (workers_ < want && workers_ < max_workers_) {
+      try {
+        std::thread([this] { work(); }).detach();
+      } catch (...) {
+        break;
+      }
       ++workers_;
     }
+    return workers_;
   }
   void work() {
     for (;;) {
@@ -371,6 +388,7 @@ class CopyPool {
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
   size_t workers_ = 0;
+  const size_t max_workers_;
 };
 
 }  // namespace plan

@@ -319,6 +319,19 @@ static void test_copy_pool() {
   auto empty = pool->submit({});
   CHECK(empty->wait() == 0);
   pool->run({});
+  // no worker can be started (a system that refuses threads, here a pool capped at 0):
+  // both forms run every piece on the caller and return with it done
+  CopyPool none(0);
+  std::vector<int> hit(5, 0);
+  std::vector<std::function<void()>> rp;
+  for (int i = 0; i < 5; ++i) rp.emplace_back([&hit, i] { ++hit[i]; });
+  none.run(rp);
+  std::vector<std::function<int()>> sp;
+  for (int i = 0; i < 5; ++i) sp.emplace_back([&hit, i] { ++hit[i]; return i == 3 ? -7 : 0; });
+  auto tk = none.submit(std::move(sp));
+  CHECK(tk->wait() == -7);
+  for (int i = 0; i < 5; ++i) CHECK(hit[i] == 2);
+  CHECK(none.workers() == 0);
   printf("copy pool: %zu workers, 16 threads x 300 batches\n", pool->workers());
 }
 
