@@ -48,7 +48,8 @@ def _u64(t):
 
 
 def _dev(torch, a):
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a if a.flags.writeable else a.copy()).cuda()
 
 
 @pytest.mark.parametrize("kernel", [hb.KERNEL_AUTO, hb.KERNEL_FIXED16, hb.KERNEL_GENERIC, hb.KERNEL_SPAN])
