@@ -856,6 +856,70 @@ def time_workload(w, steps, warmup, repeats, dist, dist_dev, warmup_min_s=WARMUP
 # ---------------------------------------------------------------------------
 # host-inclusive rate: keys start and hashes end in host memory
 # ---------------------------------------------------------------------------
+PCIE_MB = 160  # bytes per direction of the PCIe ceiling copies
+
+
+def pcie_ceilings(dev, mb=PCIE_MB, reps=5):
+    """The PCIe ceiling of this box, measured in the same run as the host lines
+    it bounds: hipMemcpyAsync (torch copy_, non_blocking) of `mb` MB between
+    page-locked host memory and HBM, host -> device alone, device -> host alone,
+    and both at once on two streams (each direction timed by HIP events on its
+    own stream), plus the HIP runtime's own pageable host -> device copy (the
+    path pageable fixed-length keys take). GB/s (1e9 B/s), median of `reps`
+    after one untimed copy of each."""
+    import torch
+
+    nb = mb * 1_000_000
+    h_src = torch.empty(nb, dtype=torch.uint8).pin_memory()
+    h_dst = torch.empty(nb, dtype=torch.uint8).pin_memory()
+    h_pg = torch.from_numpy(np.ones(nb, dtype=np.uint8))  # pageable
+    d_a = torch.empty(nb, dtype=torch.uint8, device=dev)
+    d_b = torch.empty(nb, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def one(copies):  # copies: [(stream, dst, src)] started together; ms per copy, on its own stream
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in copies]
+        torch.cuda.synchronize(dev)
+        for (st, dst, src), (a, b) in zip(copies, evs):
+            with torch.cuda.stream(st):
+                a.record(st)
+                dst.copy_(src, non_blocking=True)
+                b.record(st)
+        torch.cuda.synchronize(dev)
+        return [a.elapsed_time(b) for a, b in evs]
+
+    def med(copies):
+        one(copies)
+        runs = [one(copies) for _ in range(reps)]
+        return [float(np.median([r[i] for r in runs])) for i in range(len(copies))]
+
+    gbs = lambda ms: nb / (ms * 1e-3) / 1e9  # noqa: E731
+    h2d, = med([(s1, d_a, h_src)])
+    d2h, = med([(s2, h_dst, d_b)])
+    both_h2d, both_d2h = med([(s1, d_a, h_src), (s2, h_dst, d_b)])
+    pg = []
+    for _ in range(reps + 1):  # the runtime's pageable copy holds the calling thread: wall clock
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        d_a.copy_(h_pg)
+        torch.cuda.synchronize(dev)
+        pg.append(time.perf_counter() - t0)
+    return {"h2d": round(gbs(h2d), 2), "d2h": round(gbs(d2h), 2),
+            "both_h2d": round(gbs(both_h2d), 2), "both_d2h": round(gbs(both_d2h), 2),
+            "both": round(2 * nb / (max(both_h2d, both_d2h) * 1e-3) / 1e9, 2),
+            "h2d_pageable": round(nb / float(np.median(pg[1:])) / 1e9, 2),
+            "bytes_per_copy": nb}
+
+
+def pcie_bound(ceil, bytes_in, bytes_out):
+    """Keys/s the PCIe ceilings allow a line moving bytes_in host -> device and
+    bytes_out device -> host per key: no faster than either direction alone,
+    nor than both directions' aggregate when they run at once."""
+    t = max(bytes_in / (ceil["h2d"] * 1e9), bytes_out / (ceil["d2h"] * 1e9),
+            (bytes_in + bytes_out) / (ceil["both"] * 1e9))
+    return 1.0 / t
+
+
 def time_host_inclusive(args, dev):
     """Host buffers in and out (SHF_HASH_MEM_HOST): H2D keys (+ offsets) +
     kernel + D2H hashes, pipelined in SHF_HB_STAGE_MB chunks, SHF_HB_SLOTS in
@@ -878,8 +942,13 @@ def time_host_inclusive(args, dev):
                                      "*_pageable = pageable buffers through the pipeline (fixed-length keys by the "
                                      "runtime's pageable copy, variable-length ones staged on the CPU; the library "
                                      "never page-locks a caller's pageable memory); *_x16 = 16 threads, one slice each, "
-                                     "at once (one staging pool)"
+                                     "at once (one staging pool); uid16_* = 8-B UID parts back instead of 16-B hashes "
+                                     "(shf_uid_parts_batch_fixed). Per line: wire_bytes per key (in + out over PCIe), "
+                                     "pcie_bound = keys/s the same run's PCIe ceilings allow those bytes "
+                                     "(bench.py pcie_bound), frac_of_pcie = value / pcie_bound"
                                      % n}
+    ceil = pcie_ceilings(dev)
+    res["ceilings_gbs"] = ceil
 
     def _staged(fn, var="SHF_HB_ZERO_COPY_MAX_KEY"):  # through the copy-engine pipeline (zero copy off)
         old = os.environ.get(var)
@@ -917,6 +986,8 @@ def time_host_inclusive(args, dev):
     poff = torch.from_numpy(off.view(np.int64)).pin_memory()
     vout = np.empty((n, 2), dtype=np.uint64)
     vpo = torch.empty((n, 2), dtype=torch.int64).pin_memory()
+    uout = np.empty(n, dtype=np.uint64)
+    upo = torch.empty(n, dtype=torch.int64).pin_memory()
     cases = [
         ("fixed16_pageable", lambda: lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, SEED, out.ctypes.data,
                                                               hb.MEM_HOST), 5),
@@ -932,7 +1003,17 @@ def time_host_inclusive(args, dev):
         # hash a 1/16 slice of the same pageable batch at once, sharing the one staging pool
         ("fixed16_pageable_x16", lambda: _threaded(16, lambda lo, hi: lib.shf_hash_batch_fixed(
             keys.ctypes.data + lo * 16, 16, hi - lo, SEED, out.ctypes.data + lo * 16, hb.MEM_HOST)), 5),
+        # 8-B UID parts (the bits shf.c:800-803 reads) back instead of the 16-B hash
+        ("uid16_pageable", lambda: lib.shf_uid_parts_batch_fixed(keys.ctypes.data, 16, n, SEED, uout.ctypes.data,
+                                                                 hb.MEM_HOST), 5),
+        ("uid16_pinned", lambda: lib.shf_uid_parts_batch_fixed(pk.data_ptr(), 16, n, SEED, upo.data_ptr(),
+                                                               hb.MEM_HOST), 5),
+        ("uid16_pinned_staged", lambda: _staged(lambda: lib.shf_uid_parts_batch_fixed(pk.data_ptr(), 16, n, SEED,
+                                                                                      upo.data_ptr(), hb.MEM_HOST)),
+         5),
     ]
+    mean_len = float(off[-1]) / n
+    wire = {"fixed16": (16, 16), "var": (mean_len + 8, 16), "uid16": (16, 8)}  # (host->device, device->host) B/key
     for name, fn, reps in cases:
         rc = fn()
         if rc:
@@ -946,6 +1027,10 @@ def time_host_inclusive(args, dev):
                 raise hb.ShfHashBatchError(rc, "host-inclusive " + name)
         res[name] = {"value": n / float(np.median(ts)), "value_min": n / max(ts), "value_max": n / min(ts),
                      "repeats": reps}
+        b_in, b_out = wire[name.split("_")[0]]
+        bound = pcie_bound(ceil, b_in, b_out)
+        res[name].update({"wire_bytes": round(b_in + b_out, 1), "pcie_bound": bound,
+                          "frac_of_pcie": round(res[name]["value"] / bound, 3)})
     # sampled check of the host outputs (the oracle is the checker)
     try:
         from oracle.oracle_py import Oracle
@@ -960,6 +1045,8 @@ def time_host_inclusive(args, dev):
         so[1:] = np.cumsum(sub_lens)
         vw = o.hash_var(sub, so)
         ok = ok and np.array_equal(vout[idx], vw) and np.array_equal(vpo.numpy().view(np.uint64)[idx], vw)
+        uw = o.uid_parts(want)
+        ok = ok and np.array_equal(uout[idx], uw) and np.array_equal(upo.numpy().view(np.uint64)[idx], uw)
         res["verified"] = bool(ok)
     except Exception as e:  # noqa: BLE001
         res["verified"] = None
@@ -1447,8 +1534,12 @@ def compact_line(full, detail_path):
     else:
         line["cpu_baseline"] = None
     hi = full.get("host_inclusive")
-    if hi:
-        line["host_inclusive"] = {k: _sig(v["value"], 4) for k, v in hi.items() if isinstance(v, dict)}
+    if hi:  # per line [keys/s, frac_of_pcie]; the PCIe ceilings (GB/s) of the same run
+        line["host_inclusive"] = {k: [_sig(v["value"], 4), v.get("frac_of_pcie")] for k, v in hi.items()
+                                  if isinstance(v, dict) and "value" in v}
+        if isinstance(hi.get("ceilings_gbs"), dict):
+            c = hi["ceilings_gbs"]
+            line["host_inclusive"]["pcie_gbs"] = {k: c[k] for k in ("h2d", "d2h", "both", "h2d_pageable") if k in c}
         line["host_inclusive"]["verified"] = hi.get("verified")
     sec, ceil = {}, {}
     for name, s in (full.get("secondary") or {}).items():

@@ -48,6 +48,17 @@
  *     batch is still hashed); the synchronous calls then return
  *     SHF_HB_ERR_ARG, and the asynchronous ones report it through
  *     shf_hash_batch_status().
+ *   - fork. The HIP runtime's state (devices, streams, page-locked memory) and
+ *     this library's staging pools and copy threads do not survive fork(). In
+ *     a child forked after its parent made any call below that can reach HIP,
+ *     every such call returns SHF_HB_ERR_FORKED at once, before any HIP call
+ *     (it never hangs and never touches the parent's runtime state); exec()
+ *     or a fresh process starts afresh. A child forked before the parent's
+ *     first call uses the library normally. The reference's load test forks
+ *     its workers (/root/reference/src/test.f.shf.c:274-336): fork them first,
+ *     then hash in each. Calls exempt (no HIP):
+ *     shf_win_order_workspace_bytes, shf_tab_part_redirect,
+ *     shf_hash_batch_last_hip_error, _strerror, _version.
  */
 #ifndef SHF_HASH_BATCH_H
 #define SHF_HASH_BATCH_H
@@ -75,6 +86,7 @@ extern "C" {
 #define SHF_HB_ERR_HIP (-3)    /* a HIP call failed; shf_hash_batch_last_hip_error() has the hipError_t */
 #define SHF_HB_ERR_NOMEM (-4)  /* device or pinned-host allocation failed */
 #define SHF_HB_ERR_ARCH (-5)   /* current device is not gfx950 (MI355X) */
+#define SHF_HB_ERR_FORKED (-6) /* this process is a fork() child of one that had used the library (see "fork") */
 
 /* Where the caller's buffers live. */
 #define SHF_HASH_MEM_DEVICE 0 /* keys, offsets and out are device (HBM) pointers */
@@ -129,7 +141,19 @@ SHF_HB_API int shf_hash_batch_var_async(const void *d_bytes, const uint64_t *d_o
 SHF_HB_API int shf_hash_batch_var_sized_async(const void *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                    uint64_t key_bytes, uint32_t seed, shf_hash128 *d_out, void *hip_stream);
 
-/* ---- UID parts instead of the 16-byte hash (8 B per key, see above) ------- */
+/* ---- UID parts instead of the 16-byte hash (8 B per key, see above) -------
+ *
+ * The bits put/get/del read (shf.c:800-803, :893-896) and nothing else: 8 B per
+ * key back instead of 16, e.g. over PCIe for host buffers. A host caller feeds
+ * them to the reference's caller-supplied-hash seam with shf_use_uid_parts()
+ * (shf_hash_batch_shf.h), which rebuilds every byte of SHF_HASH that shf.c reads.
+ * Synchronous forms: mem = SHF_HASH_MEM_DEVICE or SHF_HASH_MEM_HOST, as
+ * shf_hash_batch_fixed / _var (same staging pool, copy threads, variable-length
+ * checks and status codes); parts = n words. */
+SHF_HB_API int shf_uid_parts_batch_fixed(const void *keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                         uint64_t *parts, int mem);
+SHF_HB_API int shf_uid_parts_batch_var(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
+                                       uint64_t *parts, int mem);
 
 SHF_HB_API int shf_uid_parts_batch_fixed_async(const void *d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                     uint64_t *d_parts, void *hip_stream);

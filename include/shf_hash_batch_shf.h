@@ -10,8 +10,13 @@
  * this header packages that seam:
  *
  *   shf_use_hash()           the three assignments, from one shf_hash128 record
+ *   shf_use_uid_parts()      the same from an 8-B UID-parts word
+ *                            (shf_uid_parts_batch_*): the SHF_HASH bytes shf.c
+ *                            reads, rebuilt; put/get/del behave identically
  *   shf_put_batch_var()      INTEGRATION.md §3: hash a host batch on the GPU,
  *                            then shf_put_key_val() per key
+ *   shf_put_batch_var_parts()  the same with UID parts: 8 B per key back
+ *                            from the GPU instead of 16
  *   shf_get_batch_probed()   INTEGRATION.md §6: a get batch driven by row
  *                            pre-probe records, falling back to the ordinary
  *                            get with the batch hash
@@ -52,6 +57,26 @@ static inline void shf_use_hash(const char *key, uint32_t key_len, const shf_has
     shf_hash_key_len = key_len;
 }
 
+/* shf_make_hash(key, key_len) from a UID-parts word (shf_uid_parts_batch_*,
+ * shf_hash_batch.h): put and find read only SHF_HASH.u16[0] % 256 (win),
+ * u16[1] % 2048 (tab2), u16[2] % 512 (row) and u32[2] % 2^21 (rnd)
+ * (/root/reference/src/shf.c:800-803, :893-896), so those four fields get the
+ * parts' values and every other byte is 0: each put/get/del then takes the same
+ * window, tab, row and rnd -- the same store bytes and shf_uid -- as with the
+ * full hash. (Anything else reading shf_hash -- only a debug build's trace,
+ * shf.c:461 -- sees the zeros.) The key pointer is kept, as by shf_use_hash. */
+static inline void shf_use_uid_parts(const char *key, uint32_t key_len, uint64_t parts)
+{
+    shf_hash.u64[0] = 0;
+    shf_hash.u64[1] = 0;
+    shf_hash.u16[0] = (uint16_t)SHF_UID_PARTS_WIN(parts);
+    shf_hash.u16[1] = (uint16_t)SHF_UID_PARTS_TAB(parts);
+    shf_hash.u16[2] = (uint16_t)SHF_UID_PARTS_ROW(parts);
+    shf_hash.u32[2] = SHF_UID_PARTS_RND(parts);
+    shf_hash_key = key;
+    shf_hash_key_len = key_len;
+}
+
 /* Put n host keys (key i = bytes[offsets[i] .. offsets[i+1])) with values
  * (value i = vals[val_offsets[i] .. val_offsets[i+1])): one GPU batch hash
  * (shf_hash_batch_var, SHF_HASH_MEM_HOST, seed 12345), then the reference's
@@ -77,6 +102,34 @@ static inline int64_t shf_put_batch_var(SHF *shf, const char *bytes, const uint6
             break;
     }
     free(h);
+    return (int64_t)i;
+}
+
+/* shf_put_batch_var() with UID parts: one GPU batch (shf_uid_parts_batch_var,
+ * SHF_HASH_MEM_HOST: 8 B per key back over PCIe), then shf_use_uid_parts() +
+ * shf_put_key_val() per key; the store ends byte for byte as after
+ * shf_put_batch_var(). uids_out (optional, n entries): shf_uid after each put.
+ * Returns as shf_put_batch_var(). */
+static inline int64_t shf_put_batch_var_parts(SHF *shf, const char *bytes, const uint64_t *offsets, uint64_t n,
+                                              const char *vals, const uint64_t *val_offsets, uint32_t *uids_out)
+{
+    if (n == 0) return 0;
+    uint64_t *parts = (uint64_t *)malloc(n * sizeof *parts);
+    if (!parts) return SHF_HB_ERR_NOMEM;
+    const int rc = shf_uid_parts_batch_var(bytes, offsets, n, SHF_HASH_BATCH_SEED, parts, SHF_HASH_MEM_HOST);
+    if (rc != SHF_HB_OK) {
+        free(parts);
+        return rc;
+    }
+    uint64_t i = 0;
+    for (; i < n; ++i) {
+        shf_use_uid_parts(bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]), parts[i]);
+        if (shf_put_key_val(shf, vals + val_offsets[i], (uint32_t)(val_offsets[i + 1] - val_offsets[i])) !=
+            SHF_RET_KEY_PUT)
+            break;
+        if (uids_out) uids_out[i] = shf_uid;
+    }
+    free(parts);
     return (int64_t)i;
 }
 

@@ -17,6 +17,9 @@
  *
  *   shf_hash_batch::UseHash()    MakeHash(key, key_len) with the hash already
  *                                computed (one shf_hash128 record)
+ *   shf_hash_batch::UseUidParts()  the same from an 8-B UID-parts word
+ *                                (shf_uid_parts_batch_*): the SHF_HASH fields
+ *                                shf.c reads, every other byte 0
  *   shf_hash_batch::HashVar()    a host batch of variable-length keys hashed on
  *   shf_hash_batch::HashFixed()  the GPU into a std::vector of records
  *   shf_hash_batch::PutBatch()   HashVar + UseHash + SharedHashFile::PutKeyVal
@@ -50,6 +53,21 @@ inline void UseHash(const char *key, uint32_t key_len, const shf_hash128 &h)
 {
     shf_hash.u64[0] = h.h1;
     shf_hash.u64[1] = h.h2;
+    shf_hash_key = key;
+    shf_hash_key_len = key_len;
+}
+
+/* MakeHash(key, key_len) from a UID-parts word: win, tab2, row and rnd in the
+ * SHF_HASH fields put/find read (/root/reference/src/shf.c:800-803, :893-896),
+ * zeros elsewhere; the class calls that follow behave as with the full hash. */
+inline void UseUidParts(const char *key, uint32_t key_len, uint64_t parts)
+{
+    shf_hash.u64[0] = 0;
+    shf_hash.u64[1] = 0;
+    shf_hash.u16[0] = (uint16_t)SHF_UID_PARTS_WIN(parts);
+    shf_hash.u16[1] = (uint16_t)SHF_UID_PARTS_TAB(parts);
+    shf_hash.u16[2] = (uint16_t)SHF_UID_PARTS_ROW(parts);
+    shf_hash.u32[2] = SHF_UID_PARTS_RND(parts);
     shf_hash_key = key;
     shf_hash_key_len = key_len;
 }

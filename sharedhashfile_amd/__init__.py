@@ -25,6 +25,7 @@ ERR_NODEV = -2
 ERR_HIP = -3
 ERR_NOMEM = -4
 ERR_ARCH = -5
+ERR_FORKED = -6  # a fork() child of a process that had used the library (include/shf_hash_batch.h "fork")
 
 MEM_DEVICE = 0
 MEM_HOST = 1
@@ -71,6 +72,8 @@ _SIGS = {
     "shf_hash_batch_fixed_async": [_VP, _U32, _U64, _U32, _VP, _VP],
     "shf_hash_batch_var": [_VP, _VP, _U64, _U32, _VP, _INT],
     "shf_hash_batch_var_async": [_VP, _VP, _U64, _U32, _VP, _VP],
+    "shf_uid_parts_batch_fixed": [_VP, _U32, _U64, _U32, _VP, _INT],
+    "shf_uid_parts_batch_var": [_VP, _VP, _U64, _U32, _VP, _INT],
     "shf_uid_parts_batch_fixed_async": [_VP, _U32, _U64, _U32, _VP, _VP],
     "shf_uid_parts_batch_var_async": [_VP, _VP, _U64, _U32, _VP, _VP],
     "shf_hash_batch_fixed_multi": [_VP, _U32, _U64, _U32, _VP, _INT],
@@ -688,6 +691,31 @@ def hash_fixed_host(keys, key_len=None, seed=SEED, n_devices=None):
     else:
         rc = lib.shf_hash_batch_fixed_multi(keys.ctypes.data, key_len, n, seed, out.ctypes.data, n_devices)
         _check(rc, "shf_hash_batch_fixed_multi")
+    return out
+
+
+def uid_parts_fixed_host(keys, key_len=None, seed=SEED):
+    """Host keys in, host uint64[n] UID parts out (shf_uid_parts_batch_fixed,
+    SHF_HASH_MEM_HOST: 8 B per key back instead of 16)."""
+    keys = _np_u8(keys)
+    if key_len is None:
+        n, key_len = keys.shape
+    else:
+        n = keys.size // key_len if key_len else 0
+    out = np.empty(n, dtype=np.uint64)
+    _check(load().shf_uid_parts_batch_fixed(keys.ctypes.data, key_len, n, seed, out.ctypes.data, MEM_HOST),
+           "shf_uid_parts_batch_fixed")
+    return out
+
+
+def uid_parts_var_host(data, offsets, seed=SEED):
+    """Variable-length host keys in, host uint64[n] UID parts out (shf_uid_parts_batch_var, SHF_HASH_MEM_HOST)."""
+    data = _np_u8(data)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = max(offsets.size - 1, 0)
+    out = np.empty(n, dtype=np.uint64)
+    _check(load().shf_uid_parts_batch_var(data.ctypes.data, offsets.ctypes.data, n, seed, out.ctypes.data, MEM_HOST),
+           "shf_uid_parts_batch_var")
     return out
 
 

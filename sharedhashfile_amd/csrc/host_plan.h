@@ -27,6 +27,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -40,16 +41,17 @@ constexpr size_t kHashBytes = 16, kProbeBytes = 16, kOffBytes = 8;
 inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 
 // Byte offsets of one chunk's buffers inside a slot arena: keys at 0, then the
-// hash records, the probe records (when asked) and the cnt + 1 offsets (when asked).
+// output records (rec bytes each: 16-B hashes, or 8-B UID parts), the probe
+// records (when asked) and the cnt + 1 offsets (when asked).
 struct SlotLayout {
   size_t out = 0, probe = 0, off = 0, end = 0;
 };
 
-inline SlotLayout slot_layout(size_t in_bytes, uint64_t cnt, bool probe, bool offsets) {
+inline SlotLayout slot_layout(size_t in_bytes, uint64_t cnt, bool probe, bool offsets, size_t rec = kHashBytes) {
   SlotLayout l;
   size_t o = align_up(in_bytes);
   l.out = o;
-  o += align_up((size_t)cnt * kHashBytes);
+  o += align_up((size_t)cnt * rec);
   l.probe = o;
   if (probe) o += align_up((size_t)cnt * kProbeBytes);
   l.off = o;
@@ -61,9 +63,9 @@ inline SlotLayout slot_layout(size_t in_bytes, uint64_t cnt, bool probe, bool of
 // Most fixed-length keys of key_len bytes one slot of slot_bytes holds with
 // their records; 0 when not even one does (the key then goes through a
 // temporary device buffer of its own).
-inline uint64_t fixed_chunk_keys(size_t slot_bytes, uint32_t key_len, bool probe) {
-  const size_t per = (size_t)key_len + kHashBytes + (probe ? kProbeBytes : 0);
-  auto fits = [&](uint64_t c) { return slot_layout((size_t)c * key_len, c, probe, false).end <= slot_bytes; };
+inline uint64_t fixed_chunk_keys(size_t slot_bytes, uint32_t key_len, bool probe, size_t rec = kHashBytes) {
+  const size_t per = (size_t)key_len + rec + (probe ? kProbeBytes : 0);
+  auto fits = [&](uint64_t c) { return slot_layout((size_t)c * key_len, c, probe, false, rec).end <= slot_bytes; };
   if (!fits(1)) return 0;
   // within a few keys of the answer (the regions' alignment costs at most 3 x kAlign bytes)
   uint64_t c = slot_bytes > 3 * kAlign ? std::max<uint64_t>(1, (slot_bytes - 3 * kAlign) / per) : 1;
@@ -86,12 +88,14 @@ inline uint64_t even_chunk(uint64_t n, uint64_t most) {
 // A single key too long for the slot gives i1 = i0 + 1 with *alone = true: its
 // bytes go through a temporary device buffer, its record and offsets through the slot.
 inline uint64_t var_chunk_end(const uint64_t* offsets, uint64_t i0, uint64_t n, size_t slot_bytes, bool probe,
-                              bool* alone) {
+                              bool* alone, size_t rec = kHashBytes) {
   const uint64_t base = offsets[i0];
   // each key costs at least its record and offset: no chunk holds more keys than this
-  const uint64_t cap = std::max<uint64_t>(1, slot_bytes / (kHashBytes + kOffBytes));
+  const uint64_t cap = std::max<uint64_t>(1, slot_bytes / (rec + kOffBytes));
   uint64_t lo = i0 + 1, hi = std::min(n, i0 + std::min(cap, n - i0));
-  auto fits = [&](uint64_t i1) { return slot_layout(offsets[i1] - base, i1 - i0, probe, true).end <= slot_bytes; };
+  auto fits = [&](uint64_t i1) {
+    return slot_layout(offsets[i1] - base, i1 - i0, probe, true, rec).end <= slot_bytes;
+  };
   *alone = !fits(lo);
   if (*alone) return lo;
   // largest i1 in [lo, hi] that fits (fits() is monotone: offsets never decrease)
@@ -107,8 +111,9 @@ inline uint64_t var_chunk_end(const uint64_t* offsets, uint64_t i0, uint64_t n, 
 
 // About how many chunks var_chunk_end cuts a batch of n keys and key_bytes bytes
 // into (at least 1): what a call asks the pool for, no more slots than it can use.
-inline uint64_t var_chunks_estimate(uint64_t key_bytes, uint64_t n, size_t slot_bytes, bool probe) {
-  const uint64_t per_key = kHashBytes + kOffBytes + (probe ? kProbeBytes : 0);
+inline uint64_t var_chunks_estimate(uint64_t key_bytes, uint64_t n, size_t slot_bytes, bool probe,
+                                    size_t rec = kHashBytes) {
+  const uint64_t per_key = rec + kOffBytes + (probe ? kProbeBytes : 0);
   const uint64_t room = slot_bytes > 4 * kAlign ? slot_bytes - 4 * kAlign : 1;
   uint64_t need = 0;
   if (__builtin_mul_overflow(n, per_key, &need) || __builtin_add_overflow(need, key_bytes, &need)) return UINT64_MAX;
@@ -302,6 +307,17 @@ struct Ticket {
 // parks on the queue between batches (the library keeps one pool for the
 // process's life). submit() returns at once with a Ticket; run() runs
 // pieces[0] on the caller and returns when every piece has run.
+//
+// fork(): a child has only the forking thread, so the parent's workers do not
+// exist there. The pool's pthread_atfork handlers (fork_prepare / fork_parent /
+// fork_child, registered by whoever owns the pool) hold the queue's lock across
+// the fork, so the child inherits a consistent queue; the child then drops the
+// queued pieces (their callers are not in the child), forgets the workers, makes
+// a fresh condition variable (the old one may count waiters that are gone) and
+// never starts a worker again: every later piece runs on its caller. Without
+// this a child's run() queued its pieces to workers that do not exist and
+// waited on its latch forever (the reference forks its load-test
+// workers, /root/reference/src/test.f.shf.c:274-336).
 class CopyPool {
  public:
   explicit CopyPool(size_t max_workers = (size_t)-1) : max_workers_(max_workers) {}
@@ -310,15 +326,17 @@ class CopyPool {
     auto t = std::make_shared<Ticket>();
     t->left = pieces.size();
     if (pieces.empty()) return t;
+    bool queued = false;
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (grow(pieces.size())) {
         for (auto& f : pieces) q_.push_back([t, f] { t->done(f()); });
         pieces.clear();
+        queued = true;
       }
     }
     for (auto& f : pieces) t->done(f());  // no worker could be started: on the caller, now
-    cv_.notify_all();
+    if (queued) cv_.notify_all();
     return t;
   }
 
@@ -358,10 +376,31 @@ class CopyPool {
     return workers_;
   }
 
+  // pthread_atfork handlers (see the class comment). fork_prepare runs in the
+  // forking thread before fork(), fork_parent after it in the parent,
+  // fork_child in the child (where only the forking thread exists).
+  void fork_prepare() { mu_.lock(); }
+  void fork_parent() { mu_.unlock(); }
+  void fork_child() {
+    // the queued pieces belong to callers that are not in this process: dropped
+    // without running (nobody here waits for their Tickets or latches)
+    q_.clear();
+    workers_ = 0;
+    forked_ = true;
+    new (&cv_) std::condition_variable();  // the inherited one may count waiters that do not exist here
+    mu_.unlock();
+  }
+  bool forked() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return forked_;
+  }
+
  private:
   // Under mu_: starts workers up to `want`; returns how many there are (a thread the
-  // system refuses is left out, and what is queued runs on those that exist).
+  // system refuses is left out, and what is queued runs on those that exist). A
+  // forked child starts none: its pieces run on their callers.
   size_t grow(size_t want) {
+    if (forked_) return 0;
     while (workers_ < want && workers_ < max_workers_) {
       try {
         std::thread([this] { work(); }).detach();
@@ -389,6 +428,7 @@ class CopyPool {
   std::deque<std::function<void()>> q_;
   size_t workers_ = 0;
   const size_t max_workers_;
+  bool forked_ = false;
 };
 
 }  // namespace plan

@@ -7,6 +7,7 @@
 // kernel / D2H overlapped on one stream per chunk in flight) and the multi-GPU split.
 // There is deliberately no CPU path: without a gfx950 device every call fails loudly.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -14,6 +15,7 @@
 
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -251,10 +253,7 @@ void park_ctx(DevCtx* c) {
 // The calling thread's contexts, one per device; parked for reuse when it exits.
 struct ThreadCtxs {
   std::map<int, DevCtx*> m;
-  ~ThreadCtxs() {
-    for (auto& kv : m) park_ctx(kv.second);
-    m.clear();
-  }
+  ~ThreadCtxs();
 };
 thread_local ThreadCtxs tls_ctx;
 
@@ -404,9 +403,63 @@ size_t copy_threads() {
 using shfhb::plan::CopyPool;
 using shfhb::plan::Ticket;
 
+std::atomic<CopyPool*> g_copy_pool{nullptr};
+
 CopyPool& copy_pool() {
-  static CopyPool* p = new CopyPool();
+  static CopyPool* p = [] {
+    CopyPool* q = new CopyPool();
+    g_copy_pool.store(q);
+    return q;
+  }();
   return *p;
+}
+
+// fork() (include/shf_hash_batch.h, "fork"): the HIP runtime's device state,
+// streams, pinned memory and this library's staging pools and copy workers do
+// not survive into a child. A child forked after this process used the library
+// gets SHF_HB_ERR_FORKED from every entry point, before any HIP call (instead
+// of undefined behaviour in the runtime or a wait on copy workers the child does
+// not have); the copy pool's own handlers (host_plan.h CopyPool) keep its queue
+// consistent across the fork. A child forked before any use is a fresh process
+// for the library. The reference's own load test forks its workers
+// (/root/reference/src/test.f.shf.c:274-336): fork them first, then hash.
+std::atomic<bool> g_used{false}, g_forked{false};
+CopyPool* g_fork_locked = nullptr;  // the pool fork_prepare locked (only the forking thread touches it)
+
+void atfork_prepare() {
+  g_fork_locked = g_copy_pool.load();
+  if (g_fork_locked) g_fork_locked->fork_prepare();
+}
+void atfork_parent() {
+  if (g_fork_locked) g_fork_locked->fork_parent();
+  g_fork_locked = nullptr;
+}
+void atfork_child() {
+  if (g_used.load(std::memory_order_relaxed)) g_forked.store(true, std::memory_order_relaxed);
+  if (g_fork_locked) g_fork_locked->fork_child();
+  g_fork_locked = nullptr;
+}
+[[maybe_unused]] const int g_atfork_registered = pthread_atfork(atfork_prepare, atfork_parent, atfork_child);
+
+// First statement of every entry point that may reach HIP.
+inline int enter() {
+  if (g_forked.load(std::memory_order_relaxed)) return SHF_HB_ERR_FORKED;
+  if (!g_used.load(std::memory_order_relaxed)) g_used.store(true, std::memory_order_relaxed);
+  return SHF_HB_OK;
+}
+#define HB_ENTER()                       \
+  do {                                   \
+    const int entered_ = enter();        \
+    if (entered_ != SHF_HB_OK) return entered_; \
+  } while (0)
+
+// A thread's exit parks its contexts for reuse -- except in a forked child,
+// where they are the parent's (and the lock that guards the parked ones may
+// have been held by a thread the child does not have).
+ThreadCtxs::~ThreadCtxs() {
+  if (g_forked.load(std::memory_order_relaxed)) return;
+  for (auto& kv : m) park_ctx(kv.second);
+  m.clear();
 }
 
 // Staging copies with non-temporal stores: the destination of every staging
@@ -445,21 +498,27 @@ void par_memcpy(void* dst, const void* src, size_t n) {
   copy_pool().run(pieces);
 }
 
-// What a host pipeline writes: hashes and/or row pre-probe records.
+// What a host pipeline writes: hash records (16-B SHF_HASH, or 8-B UID parts)
+// and/or row pre-probe records.
 struct HostJob {
-  shf_hash128* hash = nullptr;
-  shf_hash128* hash_dev = nullptr;  // device address of `hash` (page-locked): the kernel stores there
-  bool stage_direct = false;         // else (pageable `hash`): the kernel stores into the slot's pinned staging
+  void* hash = nullptr;      // the caller's records, rec() bytes per key
+  void* hash_dev = nullptr;  // device address of `hash` (page-locked): the kernel stores there
+  bool uid = false;          // 8-B UID parts (kOutUid: the bits shf.c:800-803 reads) instead of 16-B records
+  bool stage_direct = false;  // else (pageable `hash`): the kernel stores into the slot's pinned staging
   shf_probe* probe = nullptr;
   const shf_row_index* index = nullptr;  // with probe
   uint8_t* wins = nullptr;  // device: the batch's window bytes (kOutHashWin), key i's at wins[i]
+  size_t rec() const { return uid ? sizeof(uint64_t) : sizeof(shf_hash128); }
+  uint8_t* at(void* p, uint64_t i) const { return static_cast<uint8_t*>(p) + i * rec(); }
+  int hash_mode() const { return uid ? shfhb::kOutUid : shfhb::kOutHash; }
 };
 
 // One chunk in flight per slot; where its results go once the slot's event fires.
 struct Pending {
   bool busy = false;
-  shf_hash128* hash = nullptr;  // nullptr: not requested, or DMA'd / stored straight to the caller
-  const shf_hash128* hash_src = nullptr;  // the slot's pinned records to copy from
+  void* hash = nullptr;            // nullptr: not requested, or DMA'd / stored straight to the caller
+  const void* hash_src = nullptr;  // the slot's pinned records to copy from
+  size_t rec = sizeof(shf_hash128);  // bytes per record
   shf_probe* probe = nullptr;
   const shf_probe* probe_src = nullptr;
   uint64_t count = 0;
@@ -519,7 +578,7 @@ int drain_slot(Slot* s, Pending& p) {
   const double t0 = tr ? now_ms() : 0;
   HB_TRY(hipEventSynchronize(s->done));
   const double t1 = tr ? now_ms() : 0;
-  if (p.hash) par_memcpy(p.hash, p.hash_src, p.count * sizeof(shf_hash128));
+  if (p.hash) par_memcpy(p.hash, p.hash_src, p.count * p.rec);
   if (p.probe) par_memcpy(p.probe, p.probe_src, p.count * sizeof(shf_probe));
   if (tr) {
     tls_trace.wait += t1 - t0;
@@ -556,7 +615,7 @@ void drain_async(Slot* s, Pending& p) {
       });
     }
   };
-  if (p.hash) split(p.hash, p.hash_src, p.count * sizeof(shf_hash128));
+  if (p.hash) split(p.hash, p.hash_src, p.count * p.rec);
   if (p.probe) split(p.probe, p.probe_src, p.count * sizeof(shf_probe));
   p.copy_out = copy_pool().submit(std::move(pieces));
 }
@@ -572,7 +631,7 @@ int drain_all(Lease& L, Pending* pend) {
 // One chunk's buffers inside a slot (host_plan.h slot_layout).
 struct ChunkBufs {
   uint8_t *h_in, *d_in;
-  shf_hash128 *h_out, *d_out, *hd_out;  // hd_out: device address of h_out, or null
+  uint8_t *h_out, *d_out, *hd_out;  // the chunk's records; hd_out: device address of h_out, or null
   shf_probe *h_probe, *d_probe;
   uint64_t *h_off, *d_off;
 };
@@ -581,9 +640,9 @@ ChunkBufs carve(const Slot* s, const shfhb::plan::SlotLayout& l) {
   ChunkBufs b;
   b.h_in = s->h;
   b.d_in = s->d;
-  b.h_out = reinterpret_cast<shf_hash128*>(s->h + l.out);
-  b.d_out = reinterpret_cast<shf_hash128*>(s->d + l.out);
-  b.hd_out = s->h_dev ? reinterpret_cast<shf_hash128*>(s->h_dev + l.out) : nullptr;
+  b.h_out = s->h + l.out;
+  b.d_out = s->d + l.out;
+  b.hd_out = s->h_dev ? s->h_dev + l.out : nullptr;
   b.h_probe = reinterpret_cast<shf_probe*>(s->h + l.probe);
   b.d_probe = reinterpret_cast<shf_probe*>(s->d + l.probe);
   b.h_off = reinterpret_cast<uint64_t*>(s->h + l.off);
@@ -606,9 +665,9 @@ void job_sink(const ChunkBufs& b, const HostJob& job, uint64_t i0, shfhb::Sink* 
     k->n_slots = job.index->n_slots;
     *mode = shfhb::kOutProbe;
   } else {
-    k->out = job.hash_dev ? job.hash_dev + i0 : (job.stage_direct && b.hd_out) ? b.hd_out : b.d_out;
-    *mode = shfhb::kOutHash;
-    if (job.wins) {
+    k->out = job.hash_dev ? job.at(job.hash_dev, i0) : (job.stage_direct && b.hd_out) ? b.hd_out : b.d_out;
+    *mode = job.hash_mode();
+    if (job.wins && !job.uid) {
       k->wins = job.wins + i0;
       *mode = shfhb::kOutHashWin;
     }
@@ -618,7 +677,7 @@ void job_sink(const ChunkBufs& b, const HostJob& job, uint64_t i0, shfhb::Sink* 
 // The sink of a whole-batch launch straight into the caller's records (zero copy).
 int direct_sink(const HostJob& job, void* d_out, shfhb::Sink* k) {
   *k = out_sink(d_out);
-  if (!job.wins) return shfhb::kOutHash;
+  if (!job.wins || job.uid) return job.hash_mode();
   k->wins = job.wins;
   return shfhb::kOutHashWin;
 }
@@ -630,14 +689,15 @@ int job_d2h(Slot* s, const ChunkBufs& b, const HostJob& job, uint64_t i0, uint64
   p->reset();
   p->busy = true;
   p->count = cnt;
+  p->rec = job.rec();
   if (job.hash && !job.hash_dev && job.stage_direct && !job.probe && b.hd_out) {
-    p->hash = job.hash + i0;  // the kernel stored into the slot's pinned records (job_sink): copied out by drain_slot
+    p->hash = job.at(job.hash, i0);  // the kernel stored into the slot's pinned records (job_sink): copied out by drain_slot
     p->hash_src = b.h_out;
   } else if (job.hash && !job.hash_dev) {
-    HB_TRY(hipMemcpyAsync(hash_pinned ? job.hash + i0 : b.h_out, b.d_out, cnt * sizeof(shf_hash128),
+    HB_TRY(hipMemcpyAsync(hash_pinned ? job.at(job.hash, i0) : b.h_out, b.d_out, cnt * job.rec(),
                           hipMemcpyDeviceToHost, s->st));
     if (!hash_pinned) {
-      p->hash = job.hash + i0;
+      p->hash = job.at(job.hash, i0);
       p->hash_src = b.h_out;
     }
   }
@@ -673,7 +733,7 @@ int host_fixed_big(int dev, const uint8_t* keys, uint32_t key_len, uint64_t n, u
   int rc = lease_slots(dev, 1, &L);
   if (rc) return rc;
   Slot* s = L.s[0];
-  const ChunkBufs b = carve(s, shfhb::plan::slot_layout(0, 1, job.probe != nullptr, false));
+  const ChunkBufs b = carve(s, shfhb::plan::slot_layout(0, 1, job.probe != nullptr, false, job.rec()));
   TmpDevBuf tmp;
   tmp.st = s->st;
   HB_TRY(hipMalloc(&tmp.p, key_len));
@@ -733,7 +793,7 @@ HostJob with_direct_out(const HostJob& job, uint64_t n) {
   HostJob j = job;
   const char* e = getenv("SHF_HB_DIRECT_OUT");
   if (job.hash && !job.probe && !(e && e[0] == '0')) {
-    j.hash_dev = static_cast<shf_hash128*>(host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)));
+    j.hash_dev = host_range_device_ptr(job.hash, (size_t)n * job.rec());
     j.stage_direct = !j.hash_dev;
   }
   return j;
@@ -779,7 +839,7 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   if (rc) return rc;
   if (job.hash && !job.probe && key_len && key_len <= zero_copy_max_key()) {
     void* dk = host_range_device_ptr(keys, (size_t)n * key_len);
-    void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * sizeof(shf_hash128)) : nullptr;
+    void* dh = dk ? host_range_device_ptr(job.hash, (size_t)n * job.rec()) : nullptr;
     if (dh) {
       shfhb::Sink dsk;
       const int dmode = direct_sink(job, dh, &dsk);
@@ -790,12 +850,13 @@ int host_fixed_run(const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t s
   }
   const bool probe = job.probe != nullptr;
   const uint64_t per = shfhb::plan::fixed_chunk_keys(std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), key_len,
-                                                     probe);
+                                                     probe, job.rec());
   if (!per) return host_fixed_big(c->dev, keys, key_len, n, seed, job);
   Lease L;  // no more slots than the batch has chunks: the rest stay free for other threads' calls
   if ((rc = lease_slots(c->dev, (int)std::min<uint64_t>((n + per - 1) / per, pipeline_slots()), &L))) return rc;
-  const uint64_t chunk = shfhb::plan::even_chunk(n, shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe));
-  const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false);
+  const uint64_t chunk =
+      shfhb::plan::even_chunk(n, shfhb::plan::fixed_chunk_keys(L.s[0]->bytes, key_len, probe, job.rec()));
+  const shfhb::plan::SlotLayout lay = shfhb::plan::slot_layout((size_t)chunk * key_len, chunk, probe, false, job.rec());
   const bool in_pinned = is_host_pinned(keys), hash_pinned = is_host_pinned(job.hash),
              probe_pinned = is_host_pinned(job.probe);
   const bool via_runtime = !in_pinned && runtime_h2d();
@@ -840,7 +901,8 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
   const bool probe = job.probe != nullptr;
   Lease L;  // about as many slots as the batch has chunks (host_plan.h var_chunks_estimate)
   const uint64_t est = shfhb::plan::var_chunks_estimate(offsets[n] - offsets[0], n,
-                                                        std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), probe);
+                                                        std::max(stage_bytes(), shfhb::plan::kMinSlotBytes), probe,
+                                                        job.rec());
   if ((rc = lease_slots(c->dev, (int)std::min<uint64_t>(est, pipeline_slots()), &L))) return rc;
   const size_t slot_bytes = L.s[0]->bytes;
   const bool in_pinned = is_host_pinned(bytes), off_pinned = is_host_pinned(offsets),
@@ -852,7 +914,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
   uint64_t idx = 0;
   for (uint64_t i0 = 0; i0 < n; ++idx) {
     bool alone = false;
-    const uint64_t i1 = shfhb::plan::var_chunk_end(offsets, i0, n, slot_bytes, probe, &alone);
+    const uint64_t i1 = shfhb::plan::var_chunk_end(offsets, i0, n, slot_bytes, probe, &alone, job.rec());
     const uint64_t cnt = i1 - i0, base = offsets[i0];
     const size_t nb = (size_t)(offsets[i1] - base);
     const int q = (int)(idx % L.n);
@@ -865,7 +927,7 @@ int host_var_run(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint
     } else if ((rc = drain_slot(s, pend[q]))) {
       return rc;
     }
-    const ChunkBufs b = carve(s, shfhb::plan::slot_layout(alone ? 0 : nb, cnt, probe, true));
+    const ChunkBufs b = carve(s, shfhb::plan::slot_layout(alone ? 0 : nb, cnt, probe, true, job.rec()));
     uint8_t* d_in = alone ? (uint8_t*)tmp.p : b.d_in;
     if (nb && !in_pinned && !alone) par_memcpy(b.h_in, bytes + base, nb);
     const uint64_t* off_src = offsets + i0;
@@ -921,6 +983,13 @@ int host_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t
 HostJob hash_job(shf_hash128* out) {
   HostJob j;
   j.hash = out;
+  return j;
+}
+
+HostJob uid_job(uint64_t* parts) {
+  HostJob j;
+  j.hash = parts;
+  j.uid = true;
   return j;
 }
 
@@ -1074,6 +1143,7 @@ extern "C" {
 
 int shf_hash_batch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
                          int mem) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   if (mem == SHF_HASH_MEM_DEVICE)
@@ -1084,6 +1154,7 @@ int shf_hash_batch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_
 
 int shf_hash_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* d_out,
                                void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   return device_fixed(d_keys, key_len, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream,
@@ -1092,6 +1163,7 @@ int shf_hash_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n,
 
 int shf_hash_batch_fixed_kernel_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                       shf_hash128* d_out, int kernel, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_out || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   if (!fixed_kernel_fits(d_keys, key_len, kernel)) return SHF_HB_ERR_ARG;
@@ -1100,6 +1172,7 @@ int shf_hash_batch_fixed_kernel_async(const void* d_keys, uint32_t key_len, uint
 
 int shf_hash_batch_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out,
                        int mem) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!out || !offsets || !bytes) return SHF_HB_ERR_ARG;
   if (mem == SHF_HASH_MEM_DEVICE) return device_var(bytes, offsets, n, seed, out_sink(out), shfhb::kOutHash, nullptr, true);
@@ -1113,6 +1186,7 @@ int shf_hash_batch_var(const void* bytes, const uint64_t* offsets, uint64_t n, u
 
 int shf_hash_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
                              shf_hash128* d_out, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false);
@@ -1120,6 +1194,7 @@ int shf_hash_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uin
 
 int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
                                     shf_hash128* d_out, int kernel, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   if (!var_kernel_valid(kernel)) return SHF_HB_ERR_ARG;
@@ -1128,6 +1203,7 @@ int shf_hash_batch_var_kernel_async(const void* d_bytes, const uint64_t* d_offse
 
 int shf_hash_batch_var_sized_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint64_t key_bytes,
                                    uint32_t seed, shf_hash128* d_out, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_out), shfhb::kOutHash, (hipStream_t)hip_stream, false,
@@ -1137,6 +1213,7 @@ int shf_hash_batch_var_sized_async(const void* d_bytes, const uint64_t* d_offset
 int shf_hash_batch_var_sized_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n,
                                           uint64_t key_bytes, uint32_t seed, shf_hash128* d_out, int kernel,
                                           void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_out || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   if (!var_kernel_valid(kernel)) return SHF_HB_ERR_ARG;
@@ -1146,6 +1223,7 @@ int shf_hash_batch_var_sized_kernel_async(const void* d_bytes, const uint64_t* d
 
 int shf_uid_parts_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                     uint64_t* d_parts, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_parts || (!d_keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   return device_fixed(d_keys, key_len, n, seed, out_sink(d_parts), shfhb::kOutUid, (hipStream_t)hip_stream,
@@ -1154,14 +1232,42 @@ int shf_uid_parts_batch_fixed_async(const void* d_keys, uint32_t key_len, uint64
 
 int shf_uid_parts_batch_var_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
                                   uint64_t* d_parts, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_parts || !d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   return device_var(d_bytes, d_offsets, n, seed, out_sink(d_parts), shfhb::kOutUid, (hipStream_t)hip_stream, false);
 }
 
+int shf_uid_parts_batch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, uint64_t* parts,
+                              int mem) {
+  HB_ENTER();
+  if (n == 0) return SHF_HB_OK;
+  if (!parts || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  if (mem == SHF_HASH_MEM_DEVICE)
+    return device_fixed(keys, key_len, n, seed, out_sink(parts), shfhb::kOutUid, nullptr, shfhb::kKernelAuto, true);
+  if (mem == SHF_HASH_MEM_HOST) return host_fixed((const uint8_t*)keys, key_len, n, seed, uid_job(parts));
+  return SHF_HB_ERR_ARG;
+}
+
+int shf_uid_parts_batch_var(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, uint64_t* parts,
+                            int mem) {
+  HB_ENTER();
+  if (n == 0) return SHF_HB_OK;
+  if (!parts || !offsets || !bytes) return SHF_HB_ERR_ARG;
+  if (mem == SHF_HASH_MEM_DEVICE)
+    return device_var(bytes, offsets, n, seed, out_sink(parts), shfhb::kOutUid, nullptr, true);
+  if (mem == SHF_HASH_MEM_HOST) {
+    const int rc = check_var_lengths_host(offsets, n);
+    if (rc) return rc;
+    return host_var((const uint8_t*)bytes, offsets, n, seed, uid_job(parts));
+  }
+  return SHF_HB_ERR_ARG;
+}
+
 int shf_hash_batch_fixed_win_kernel_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                           shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start,
                                           void* d_workspace, size_t workspace_bytes, int kernel, void* hip_stream) {
+  HB_ENTER();
   if (n == 0 && !d_win_start) return SHF_HB_OK;
   if (n && (!d_out || !d_perm || (!d_keys && key_len))) return SHF_HB_ERR_ARG;
   if (key_len > kMaxKeyLen || n > 0xffffffffull || !fixed_kernel_fits(d_keys, key_len, kernel)) return SHF_HB_ERR_ARG;
@@ -1185,6 +1291,7 @@ int shf_hash_batch_fixed_win_kernel_async(const void* d_keys, uint32_t key_len, 
 int shf_hash_batch_fixed_win_async(const void* d_keys, uint32_t key_len, uint64_t n, uint32_t seed,
                                    shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start, void* d_workspace,
                                    size_t workspace_bytes, void* hip_stream) {
+  HB_ENTER();
   return shf_hash_batch_fixed_win_kernel_async(d_keys, key_len, n, seed, d_out, d_perm, d_win_start, d_workspace,
                                                 workspace_bytes, SHF_HB_KERNEL_AUTO, hip_stream);
 }
@@ -1192,6 +1299,7 @@ int shf_hash_batch_fixed_win_async(const void* d_keys, uint32_t key_len, uint64_
 int shf_hash_batch_var_win_kernel_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
                                         shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start,
                                         void* d_workspace, size_t workspace_bytes, int kernel, void* hip_stream) {
+  HB_ENTER();
   if (n == 0 && !d_win_start) return SHF_HB_OK;
   if (n && (!d_out || !d_perm || !d_offsets || !d_bytes)) return SHF_HB_ERR_ARG;
   if (n > 0xffffffffull || !var_kernel_valid(kernel)) return SHF_HB_ERR_ARG;
@@ -1213,6 +1321,7 @@ int shf_hash_batch_var_win_kernel_async(const void* d_bytes, const uint64_t* d_o
 int shf_hash_batch_var_win_async(const void* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t seed,
                                  shf_hash128* d_out, uint32_t* d_perm, uint32_t* d_win_start, void* d_workspace,
                                  size_t workspace_bytes, void* hip_stream) {
+  HB_ENTER();
   return shf_hash_batch_var_win_kernel_async(d_bytes, d_offsets, n, seed, d_out, d_perm, d_win_start, d_workspace,
                                              workspace_bytes, SHF_HB_KERNEL_AUTO, hip_stream);
 }
@@ -1284,16 +1393,19 @@ extern "C" {
 
 int shf_hash_batch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
                              uint32_t* perm, uint32_t* win_start, int mem) {
+  HB_ENTER();
   return hash_win_sync(false, keys, nullptr, key_len, n, seed, out, perm, win_start, mem);
 }
 
 int shf_hash_batch_var_win(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out,
                            uint32_t* perm, uint32_t* win_start, int mem) {
+  HB_ENTER();
   return hash_win_sync(true, bytes, offsets, 0, n, seed, out, perm, win_start, mem);
 }
 
 int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
                                int n_devices) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!out || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   const uint8_t* k = (const uint8_t*)keys;
@@ -1304,6 +1416,7 @@ int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, u
 
 int shf_hash_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed,
                              shf_hash128* out, int n_devices) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!out || !offsets || !bytes) return SHF_HB_ERR_ARG;
   int rc = check_var_lengths_host(offsets, n);
@@ -1315,6 +1428,7 @@ int shf_hash_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_
 }
 
 int shf_row_index_create(uint64_t n_slots, shf_row_index** out) {
+  HB_ENTER();
   if (!out) return SHF_HB_ERR_ARG;
   *out = nullptr;
   if (n_slots > ((uint64_t)1 << 21)) return SHF_HB_ERR_ARG;  // slot must fit the 21 high bits of tab_slot
@@ -1340,6 +1454,7 @@ int shf_row_index_create(uint64_t n_slots, shf_row_index** out) {
 }
 
 int shf_row_index_destroy(shf_row_index* index) {
+  HB_ENTER();
   if (!index) return SHF_HB_OK;
   int prev = 0;
   (void)hipGetDevice(&prev);
@@ -1354,6 +1469,7 @@ int shf_row_index_destroy(shf_row_index* index) {
 }
 
 int shf_row_index_set_tabs(shf_row_index* index, const uint32_t* tab_slot) {
+  HB_ENTER();
   if (!index || !tab_slot) return SHF_HB_ERR_ARG;
   index->compact = false;
   HB_TRY(hipMemcpy(index->d_tab_slot, tab_slot, SHF_ROW_INDEX_TABS * sizeof(uint32_t), hipMemcpyDefault));
@@ -1369,6 +1485,7 @@ int shf_row_index_set_tabs(shf_row_index* index, const uint32_t* tab_slot) {
 }
 
 int shf_row_index_set_rows(shf_row_index* index, uint64_t first, uint64_t count, const void* rows) {
+  HB_ENTER();
   if (!index || (!rows && count) || first > index->n_slots || count > index->n_slots - first) return SHF_HB_ERR_ARG;
   if (!count) return SHF_HB_OK;
   HB_TRY(hipMemcpy(index->d_rows + first * SHF_ROW_INDEX_SLOT_BYTES, rows, count * SHF_ROW_INDEX_SLOT_BYTES,
@@ -1377,6 +1494,7 @@ int shf_row_index_set_rows(shf_row_index* index, uint64_t first, uint64_t count,
 }
 
 int shf_row_index_device_ptrs(const shf_row_index* index, uint32_t** d_tab_slot, void** d_rows, uint64_t* n_slots) {
+  HB_ENTER();
   if (!index) return SHF_HB_ERR_ARG;
   index->external = true;  // the caller may now write tab_slot: the probes read it directly
   if (d_tab_slot) *d_tab_slot = index->d_tab_slot;
@@ -1388,6 +1506,7 @@ int shf_row_index_device_ptrs(const shf_row_index* index, uint32_t** d_tab_slot,
 int shf_probe_batch_fixed_kernel_async(const shf_row_index* index, const void* d_keys, uint32_t key_len, uint64_t n,
                                        uint32_t seed, shf_hash128* d_hashes, shf_probe* d_probe, int kernel,
                                        void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if ((!d_keys && key_len) || key_len > kMaxKeyLen || !fixed_kernel_fits(d_keys, key_len, kernel))
     return SHF_HB_ERR_ARG;
@@ -1399,12 +1518,14 @@ int shf_probe_batch_fixed_kernel_async(const shf_row_index* index, const void* d
 
 int shf_probe_batch_fixed_async(const shf_row_index* index, const void* d_keys, uint32_t key_len, uint64_t n,
                                 uint32_t seed, shf_hash128* d_hashes, shf_probe* d_probe, void* hip_stream) {
+  HB_ENTER();
   return shf_probe_batch_fixed_kernel_async(index, d_keys, key_len, n, seed, d_hashes, d_probe, SHF_HB_KERNEL_AUTO,
                                             hip_stream);
 }
 
 int shf_probe_batch_var_async(const shf_row_index* index, const void* d_bytes, const uint64_t* d_offsets, uint64_t n,
                               uint32_t seed, shf_hash128* d_hashes, shf_probe* d_probe, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_offsets || !d_bytes) return SHF_HB_ERR_ARG;
   shfhb::Sink sink;
@@ -1415,6 +1536,7 @@ int shf_probe_batch_var_async(const shf_row_index* index, const void* d_bytes, c
 
 int shf_probe_batch_fixed(const shf_row_index* index, const void* keys, uint32_t key_len, uint64_t n, uint32_t seed,
                           shf_hash128* hashes, shf_probe* probes, int mem) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!probes || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
   shfhb::Sink sink;
@@ -1432,6 +1554,7 @@ int shf_probe_batch_fixed(const shf_row_index* index, const void* keys, uint32_t
 
 int shf_probe_batch_var(const shf_row_index* index, const void* bytes, const uint64_t* offsets, uint64_t n,
                         uint32_t seed, shf_hash128* hashes, shf_probe* probes, int mem) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!probes || !offsets || !bytes) return SHF_HB_ERR_ARG;
   shfhb::Sink sink;
@@ -1449,6 +1572,7 @@ int shf_probe_batch_var(const shf_row_index* index, const void* bytes, const uin
 
 int shf_probe_batch_hashes_async(const shf_row_index* index, const shf_hash128* d_hashes, uint64_t n,
                                  shf_probe* d_probe, void* hip_stream) {
+  HB_ENTER();
   if (n == 0) return SHF_HB_OK;
   if (!d_hashes) return SHF_HB_ERR_ARG;
   shfhb::Sink sink;
@@ -1463,6 +1587,7 @@ int shf_probe_batch_hashes_async(const shf_row_index* index, const shf_hash128* 
 int shf_tab_copy_batch_async(const void* d_src, uint64_t src_bytes, void* d_dst, uint64_t dst_bytes,
                              shf_tab_job* d_jobs, uint32_t n_jobs, const uint16_t* d_maps, uint32_t n_maps,
                              const shf_tab_params* params, void* hip_stream) {
+  HB_ENTER();
   if (n_jobs == 0) return SHF_HB_OK;
   if (!d_src || !d_dst || !d_jobs || !params) return SHF_HB_ERR_ARG;
   DevCtx* c = nullptr;
@@ -1475,6 +1600,7 @@ int shf_tab_copy_batch_async(const void* d_src, uint64_t src_bytes, void* d_dst,
 
 int shf_tab_copy_batch(const void* src, uint64_t src_bytes, void* dst, uint64_t dst_bytes, shf_tab_job* jobs,
                        uint32_t n_jobs, const uint16_t* maps, uint32_t n_maps, const shf_tab_params* params, int mem) {
+  HB_ENTER();
   if (n_jobs == 0) return SHF_HB_OK;
   if (!src || !dst || !jobs || !params || (mem != SHF_HASH_MEM_DEVICE && mem != SHF_HASH_MEM_HOST))
     return SHF_HB_ERR_ARG;
@@ -1516,6 +1642,7 @@ size_t shf_win_order_workspace_bytes(uint64_t n) { return (size_t)shfhb::win_ord
 
 int shf_win_order_async(const shf_hash128* d_hashes, uint64_t n, uint32_t* d_perm, uint32_t* d_win_start,
                         void* d_workspace, size_t workspace_bytes, void* hip_stream) {
+  HB_ENTER();
   if (n == 0 && !d_win_start) return SHF_HB_OK;
   if (n > 0xffffffffull) return SHF_HB_ERR_ARG;
   if (n && (!d_hashes || !d_perm || !win_workspace_ok(d_workspace, workspace_bytes, n))) return SHF_HB_ERR_ARG;
@@ -1527,6 +1654,7 @@ int shf_win_order_async(const shf_hash128* d_hashes, uint64_t n, uint32_t* d_per
 }
 
 int shf_win_order(const shf_hash128* hashes, uint64_t n, uint32_t* perm, uint32_t* win_start, int mem) {
+  HB_ENTER();
   if (mem != SHF_HASH_MEM_DEVICE && mem != SHF_HASH_MEM_HOST) return SHF_HB_ERR_ARG;
   if (n == 0 && !win_start) return SHF_HB_OK;
   if (n > 0xffffffffull || (n && (!hashes || !perm))) return SHF_HB_ERR_ARG;
@@ -1570,6 +1698,7 @@ int shf_tab_part_redirect(uint16_t* map, uint32_t tab_old, uint32_t tab_new) {
 }
 
 int shf_hash_batch_status(void* hip_stream) {
+  HB_ENTER();
   DevCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -1582,9 +1711,13 @@ int shf_hash_batch_status(void* hip_stream) {
   return *c->h_status ? SHF_HB_ERR_ARG : SHF_HB_OK;
 }
 
-int shf_hash_batch_device_count(void) { return visible_devices(); }
+int shf_hash_batch_device_count(void) {
+  HB_ENTER();
+  return visible_devices();
+}
 
 int shf_hash_batch_check_device(void) {
+  HB_ENTER();
   DevCtx* c = nullptr;
   return current_ctx(&c);
 }
@@ -1592,6 +1725,7 @@ int shf_hash_batch_check_device(void) {
 int shf_hash_batch_last_hip_error(void) { return tls_last_hip; }
 
 int shf_hash_batch_release(void) {
+  HB_ENTER();
   free_contexts();
   std::vector<Pool*> pools;
   {
@@ -1616,6 +1750,8 @@ const char* shf_hash_batch_strerror(int status) {
       return "out of device or pinned host memory";
     case SHF_HB_ERR_ARCH:
       return "device is not gfx950 (MI355X)";
+    case SHF_HB_ERR_FORKED:
+      return "forked after this process used the library: HIP state does not survive fork()";
     default:
       return "unknown status";
   }

@@ -13,6 +13,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <pthread.h>
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <random>
@@ -60,6 +65,19 @@ static void test_fixed_chunks() {
       }
   // the default slot holds the round-4 chunk of 16-B keys (8 MiB of keys)
   CHECK(fixed_chunk_keys((size_t)16 << 20, 16, false) == ((size_t)16 << 20) / 32);
+  // 8-B UID parts instead of 16-B records: a third more 16-B keys per slot, every layout inside it
+  {
+    const uint64_t c8 = fixed_chunk_keys((size_t)16 << 20, 16, false, 8);
+    CHECK(c8 <= ((size_t)16 << 20) / 24 && c8 + 64 >= ((size_t)16 << 20) / 24);
+  }
+  for (size_t slot : slots)
+    for (uint32_t L : lens) {
+      const uint64_t c = fixed_chunk_keys(slot, L, false, 8);
+      if (!c) continue;
+      const SlotLayout l = slot_layout((size_t)c * L, c, false, false, 8);
+      CHECK(l.out % kAlign == 0 && l.end % kAlign == 0 && l.end <= slot && l.probe >= l.out + c * 8);
+      CHECK(slot_layout((size_t)(c + 1) * L, c + 1, false, false, 8).end > slot);
+    }
   // even chunks: never more chunks than the slot size forces, none above it, sizes within one chunk's rounding
   for (uint64_t most : {1ull, 7ull, 512ull << 10, 1000003ull})
     for (uint64_t n : {1ull, 6ull, 7ull, 8ull, 625000ull, 10000000ull, 1000000007ull}) {
@@ -335,12 +353,83 @@ static void test_copy_pool() {
   printf("copy pool: %zu workers, 16 threads x 300 batches\n", pool->workers());
 }
 
+// fork() after the copy workers have run (the reference
+// forks up to 36 load-test workers, /root/reference/src/test.f.shf.c:274-336):
+// with the pool's pthread_atfork handlers registered, a child forked while
+// another thread keeps the workers busy finishes run() and submit() on its own
+// thread and exits 0 within a time limit, instead of waiting forever on
+// workers it does not have; the parent's pool keeps working.
+static CopyPool* g_fork_pool = nullptr;
+static void fork_prepare() { g_fork_pool->fork_prepare(); }
+static void fork_parent() { g_fork_pool->fork_parent(); }
+static void fork_child() { g_fork_pool->fork_child(); }
+
+static bool pool_round(CopyPool* pool, size_t k) {
+  std::vector<int> hits(k, 0);
+  std::vector<std::function<void()>> pieces;
+  for (size_t i = 0; i < k; ++i) pieces.emplace_back([&hits, i] { ++hits[i]; });
+  pool->run(pieces);
+  auto out = std::make_shared<std::vector<int>>(k, 0);
+  std::vector<std::function<int()>> sp;
+  for (size_t i = 0; i < k; ++i) sp.emplace_back([out, i] { ++(*out)[i]; return i == 1 ? -5 : 0; });
+  const int rc = pool->submit(std::move(sp))->wait();
+  bool ok = rc == (k > 1 ? -5 : 0);
+  for (size_t i = 0; i < k; ++i) ok = ok && hits[i] == 1 && (*out)[i] == 1;
+  return ok;
+}
+
+static void test_fork() {
+  g_fork_pool = new CopyPool();  // never destroyed, as in the library
+  CHECK(pthread_atfork(fork_prepare, fork_parent, fork_child) == 0);
+  CHECK(pool_round(g_fork_pool, 8));
+  CHECK(g_fork_pool->workers() >= 7);  // the parent has workers the child will not have
+  std::atomic<bool> stop{false};
+  std::atomic<long> busy_rounds{0};
+  std::thread busy([&] {  // the workers stay busy (queue and latches in use) across every fork
+    while (!stop.load()) {
+      if (!pool_round(g_fork_pool, 6)) ++failures;
+      ++busy_rounds;
+    }
+  });
+  for (int round = 0; round < 8; ++round) {
+    const pid_t pid = fork();
+    if (pid == 0) {
+      // the child: no workers, every piece on this thread; then the same again
+      const bool ok = g_fork_pool->forked() && pool_round(g_fork_pool, 8) && pool_round(g_fork_pool, 1) &&
+                      g_fork_pool->workers() == 0 && pool_round(g_fork_pool, 12);
+      _exit(ok ? 0 : 3);
+    }
+    CHECK(pid > 0);
+    if (pid <= 0) break;
+    int status = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const pid_t r = waitpid(pid, &status, WNOHANG);
+      if (r == pid) break;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+        kill(pid, SIGKILL);
+        waitpid(pid, &status, 0);
+        fprintf(stderr, "fork: child %d hung\n", (int)pid);
+        ++failures;
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+    CHECK(WIFEXITED(status) && WEXITSTATUS(status) == 0);
+  }
+  stop = true;
+  busy.join();
+  CHECK(!g_fork_pool->forked() && pool_round(g_fork_pool, 12));  // the parent's pool is unchanged
+  printf("fork: 8 children finished on their own thread, %ld parent rounds alongside\n", busy_rounds.load());
+}
+
 int main() {
   test_fixed_chunks();
   test_var_chunks();
   test_stream_copy();
   test_pool();
   test_copy_pool();
+  test_fork();
   if (failures) {
     fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;

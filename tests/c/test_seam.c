@@ -15,7 +15,12 @@
  *      (shf_probe_batch_var, host memory), shf_get_batch_probed(): the same
  *      answers, most stored keys served by the uid path;
  *   4. fixed 16-byte keys: shf_hash_batch_fixed + shf_use_hash + put, then
- *      the reference's get with its CPU hash finds every one.
+ *      the reference's get with its CPU hash finds every one;
+ *   5./6. the window-ordered put and window ranges;
+ *   7. 8-B UID parts (shf_uid_parts_batch_var, host memory) through
+ *      shf_use_uid_parts: a store put from parts is byte-equal to one put from
+ *      the full hashes, with the same shf_uid per key, and the reference's
+ *      own get finds every key in it.
  *
  * TEST INFRASTRUCTURE: built by tests/c/Makefile where /root/reference exists
  * (the reference's headers are needed to compile it), into tests/c/build/, which
@@ -57,6 +62,44 @@ static int remove_entry(const char *path, const struct stat *sb, int flag, struc
     (void)flag;
     (void)ftw;
     return remove(path);
+}
+
+/* Every tab file of store `a` byte-equal to the same file of store `b` (both in folder),
+ * with the same tab counts per window; the number of files compared, or -1. */
+static int64_t same_store_files(const char *folder, const char *a, SHF *sa, const char *b, SHF *sb)
+{
+    int64_t same = 0;
+    for (uint32_t win = 0; win < SHF_WINS_PER_SHF; ++win) {
+        if (sa->shf_mmap->wins[win].tabs_used != sb->shf_mmap->wins[win].tabs_used) return -1;
+        for (uint32_t tab = 0; tab < sa->shf_mmap->wins[win].tabs_used; ++tab) {
+            char pa[512], pb[512];
+            snprintf(pa, sizeof pa, "%s/%s.shf/%03u/%04u.tab", folder, a, win, tab);
+            snprintf(pb, sizeof pb, "%s/%s.shf/%03u/%04u.tab", folder, b, win, tab);
+            FILE *fa = fopen(pa, "rb"), *fb = fopen(pb, "rb");
+            if (!fa || !fb) {
+                if (fa) fclose(fa);
+                if (fb) fclose(fb);
+                return -1;
+            }
+            int ca, cb;
+            do {
+                ca = fgetc(fa);
+                cb = fgetc(fb);
+            } while (ca == cb && ca != EOF);
+            fclose(fa);
+            fclose(fb);
+            if (ca != cb) return -1;
+            ++same;
+        }
+    }
+    return same;
+}
+
+/* The UID-parts word of a full hash (shf_hash_batch.h SHF_UID_PARTS_*). */
+static uint64_t parts_of(const shf_hash128 *h)
+{
+    return (h->h1 & 0xff) | ((h->h1 >> 16) & 0x7ff) << 8 | ((h->h1 >> 32) & 0x1ff) << 19 |
+           (h->h2 & 0x1fffff) << 32;
 }
 
 static uint64_t good_values;
@@ -187,27 +230,8 @@ int main(int argc, char **argv)
         if ((h[perm[j]].h1 & 0xff) < (h[perm[j - 1]].h1 & 0xff) ||
             ((h[perm[j]].h1 & 0xff) == (h[perm[j - 1]].h1 & 0xff) && perm[j] < perm[j - 1]))
             return fail("window order: not a stable sort by window");
-    uint64_t same_files = 0;
-    for (uint32_t win = 0; win < SHF_WINS_PER_SHF; ++win) {
-        if (shf->shf_mmap->wins[win].tabs_used != wshf->shf_mmap->wins[win].tabs_used)
-            return fail("window order: tab counts differ");
-        for (uint32_t tab = 0; tab < shf->shf_mmap->wins[win].tabs_used; ++tab) {
-            char pa[512], pb[512];
-            snprintf(pa, sizeof pa, "%s/seam.shf/%03u/%04u.tab", folder, win, tab);
-            snprintf(pb, sizeof pb, "%s/seamwin.shf/%03u/%04u.tab", folder, win, tab);
-            FILE *fa = fopen(pa, "rb"), *fb = fopen(pb, "rb");
-            if (!fa || !fb) return fail("window order: tab file missing");
-            int ca, cb;
-            do {
-                ca = fgetc(fa);
-                cb = fgetc(fb);
-            } while (ca == cb && ca != EOF);
-            fclose(fa);
-            fclose(fb);
-            if (ca != cb) return fail("window order: tab files differ");
-            ++same_files;
-        }
-    }
+    const int64_t same_files = same_store_files(folder, "seam", shf, "seamwin", wshf);
+    if (same_files < 0) return fail("window order: tab files differ");
     /* a get batch (stored and absent keys) in window order gives the reference's answers */
     shf_hash128 *hw = malloc(n * sizeof *hw);
     uint32_t *permq = malloc(n * sizeof *permq);
@@ -239,13 +263,67 @@ int main(int argc, char **argv)
     if (rfound != ref_found || good_values != ref_right) return fail("window ranges: get answers differ");
     shf_detach(rshf);
 
+    /* 7. UID parts (8 B per key from the GPU) through shf_use_uid_parts: a store put from
+     *    parts ends byte for byte as one put from the full hashes, with the same shf_uid per
+     *    key, and the reference's own get (CPU shf_make_hash) finds every key in it */
+    uint64_t *parts = malloc(n * sizeof *parts);
+    if (shf_uid_parts_batch_var(bytes, off, n, SHF_HASH_BATCH_SEED, parts, SHF_HASH_MEM_HOST) != SHF_HB_OK)
+        return fail("shf_uid_parts_batch_var");
+    for (uint64_t i = 0; i < n; ++i)
+        if (parts[i] != parts_of(&h[i])) return fail("UID parts != the parts of the GPU hash");
+    SHF *hshf = shf_attach(folder, "seamuidh", 0);
+    SHF *pshf = shf_attach(folder, "seamuidp", 0);
+    if (!hshf || !pshf) return fail("shf_attach uid parts");
+    uint32_t *uid_h = malloc(n_put * sizeof *uid_h), *uid_p = malloc(n_put * sizeof *uid_p);
+    for (uint64_t i = 0; i < n_put; ++i) {
+        shf_use_hash(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), &h[i]);
+        if (shf_put_key_val(hshf, vals + voff[i], 8) != SHF_RET_KEY_PUT) return fail("uid parts: full-hash put");
+        uid_h[i] = shf_uid;
+    }
+    if (shf_put_batch_var_parts(pshf, bytes, off, n_put, vals, voff, uid_p) != (int64_t)n_put)
+        return fail("shf_put_batch_var_parts");
+    uint64_t uid_same = 0;
+    for (uint64_t i = 0; i < n_put; ++i) uid_same += uid_h[i] == uid_p[i] && uid_p[i] != SHF_UID_NONE;
+    if (uid_same != n_put) return fail("uid parts: shf_uid differs from the full-hash put");
+    const int64_t parts_same_files = same_store_files(folder, "seamuidh", hshf, "seamuidp", pshf);
+    if (parts_same_files < 0) return fail("uid parts: tab files differ from the full-hash put");
+    uint64_t pfound = 0, pright = 0;
+    for (uint64_t i = 0; i < n; ++i) {  /* the reference's own get, CPU hash */
+        shf_make_hash(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        if (shf_get_key_val_copy(pshf) == SHF_RET_KEY_FOUND) {
+            ++pfound;
+            pright += i < n_put && shf_val_len == 8 && memcmp(shf_val, &i, 8) == 0;
+        }
+    }
+    if (pfound != n_put || pright != n_put) return fail("uid parts: reference get after a parts put");
+    /* and a get with the parts in the seam gives the reference's answers too */
+    uint64_t pgot = 0, pgot_any = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        shf_use_uid_parts(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), parts[i]);
+        if (shf_get_key_val_copy(pshf) == SHF_RET_KEY_FOUND) {
+            ++pgot_any;
+            pgot += i < n_put && shf_val_len == 8 && memcmp(shf_val, &i, 8) == 0;
+        }
+    }
+    if (pgot != n_put || pgot_any != n_put) return fail("uid parts: get through shf_use_uid_parts");
+    /* fixed 16-byte keys: the parts of the fixed-length entry point */
+    uint64_t *fparts = malloc(nf * sizeof *fparts);
+    if (shf_uid_parts_batch_fixed(fk, 16, nf, SHF_HASH_BATCH_SEED, fparts, SHF_HASH_MEM_HOST) != SHF_HB_OK)
+        return fail("shf_uid_parts_batch_fixed");
+    for (uint64_t i = 0; i < nf; ++i)
+        if (fparts[i] != parts_of(&fh[i])) return fail("fixed UID parts != the parts of the GPU hash");
+    shf_detach(hshf);
+    shf_detach(pshf);
+
     printf("{\"n_put\": %llu, \"n_query\": %llu, \"ref_found\": %llu, \"ref_right\": %llu, \"probed_found\": %llu, "
-           "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu, \"win_order_same_tab_files\": %llu, "
-           "\"win_order_found\": %llu, \"win_range_put\": %lld}\n",
+           "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu, \"win_order_same_tab_files\": %lld, "
+           "\"win_order_found\": %llu, \"win_range_put\": %lld, \"parts_same_uids\": %llu, "
+           "\"parts_same_tab_files\": %lld, \"parts_ref_found\": %llu, \"parts_get_found\": %llu}\n",
            (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
            (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
-           (unsigned long long)ffound, (unsigned long long)same_files, (unsigned long long)wfound2,
-           (long long)range_put);
+           (unsigned long long)ffound, (long long)same_files, (unsigned long long)wfound2,
+           (long long)range_put, (unsigned long long)uid_same, (long long)parts_same_files,
+           (unsigned long long)pright, (unsigned long long)pgot);
     shf_detach(wshf);
     /* the stores' files go with the folder (shf_del would run `du` and `rm` through popen) */
     shf_detach(shf);

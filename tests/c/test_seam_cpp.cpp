@@ -176,12 +176,27 @@ int main(int argc, char **argv)
     }
     expect(fixed_put == nf && fixed_found == nf, "fixed 16-B keys: UseHash put, MakeHash get");
 
+    /* 4. the same keys' 8-B UID parts (shf_uid_parts_batch_fixed) through UseUidParts: GetKeyValCopy finds each */
+    std::vector<uint64_t> parts(nf);
+    uint64_t parts_found = 0;
+    if (shf_uid_parts_batch_fixed(fk.data(), 16, nf, SHF_HASH_BATCH_SEED, parts.data(), SHF_HASH_MEM_HOST) ==
+        SHF_HB_OK) {
+        for (uint64_t i = 0; i < nf; ++i) {
+            shf_hash_batch::UseUidParts(reinterpret_cast<const char *>(&fk[16 * i]), 16, parts[i]);
+            uint64_t v = ~0ull;
+            if (shf.GetKeyValCopy() == SHF_RET_KEY_FOUND && shf_val_len == 8) memcpy(&v, shf_val, 8);
+            parts_found += v == i;
+        }
+    }
+    expect(parts_found == nf, "fixed 16-B keys: UID parts through UseUidParts, GetKeyValCopy");
+
     /* the store's files go with the folder (shf_del would run `du` and `rm` through popen) */
     shf.Detach();
     nftw(folder, remove_entry, 16, FTW_DEPTH | FTW_PHYS);
     printf("{\"checks\": %d, \"failures\": %d, \"own_hash_keys\": %zu, \"n_put\": %llu, \"found\": %llu, "
-           "\"right\": %llu, \"absent_found\": %llu, \"fixed_found\": %llu}\n",
+           "\"right\": %llu, \"absent_found\": %llu, \"fixed_found\": %llu, \"parts_found\": %llu}\n",
            checks, failures, keys.size(), (unsigned long long)n_put, (unsigned long long)found,
-           (unsigned long long)right, (unsigned long long)absent_found, (unsigned long long)fixed_found);
+           (unsigned long long)right, (unsigned long long)absent_found, (unsigned long long)fixed_found,
+           (unsigned long long)parts_found);
     return failures ? 1 : 0;
 }

@@ -212,10 +212,13 @@ def test_stdout_line_fits_the_driver_tail_at_one_and_eight_ranks():
     unparsed: the stdout line is capped at 4 KB, the rest goes to the detail file."""
     cpu = {"value": 1.476e8, "unit": "keys/s", "cores": 1, "kind": "reference", "sample": "x" * 400,
            "host_cpus": {"visible": 256}, "threads16": {"value": 2.1e9, "unit": "keys/s", "cores": 16, "sample": "y"}}
-    hi = {"unit": "keys/s", "note": "n" * 500, "verified": True}
+    hi = {"unit": "keys/s", "note": "n" * 500, "verified": True,
+          "ceilings_gbs": {"h2d": 55.71, "d2h": 56.12, "both_h2d": 40.17, "both_d2h": 40.33, "both": 80.44,
+                           "h2d_pageable": 51.32, "bytes_per_copy": 160000000}}
     for k in ("fixed16_pageable", "fixed16_pinned", "fixed16_pinned_staged", "var_pageable", "var_pinned",
-              "fixed16_pageable_x16"):
-        hi[k] = {"value": 2.5e9, "value_min": 2.4e9, "value_max": 2.6e9, "repeats": 5}
+              "fixed16_pageable_x16", "uid16_pageable", "uid16_pinned", "uid16_pinned_staged"):
+        hi[k] = {"value": 2.5e9, "value_min": 2.4123e9, "value_max": 2.6123e9, "repeats": 5, "wire_bytes": 32.0,
+                 "pcie_bound": 2.51375e9, "frac_of_pcie": 0.995}
     for world in (1, 8):
         full, line = _compact(world, cpu if world == 1 else None, hi if world == 1 else None)
         s = bench.json.dumps(line)
@@ -233,9 +236,22 @@ def test_stdout_line_fits_the_driver_tail_at_one_and_eight_ranks():
         assert len(bench.json.dumps(full)) > len(s)  # the detail record keeps what the line drops
     _, line1 = _compact(1, cpu, hi)
     assert line1["cpu_baseline"]["kind"] == "reference" and line1["cpu_baseline"]["multi"]["cores"] == 16
-    assert line1["host_inclusive"]["fixed16_pinned"] == 2.5e9
+    assert line1["host_inclusive"]["fixed16_pinned"] == [2.5e9, 0.995]  # [keys/s, frac_of_pcie]
+    assert line1["host_inclusive"]["uid16_pageable"] == [2.5e9, 0.995]
+    assert line1["host_inclusive"]["pcie_gbs"] == {"h2d": 55.71, "d2h": 56.12, "both": 80.44, "h2d_pageable": 51.32}
     _, line8 = _compact(8)
     assert "per_rank" not in line8 and line8["slowest_over_fastest_rank"]["fixed16"] == round(57.0 / 50.0, 4)
+
+
+def test_pcie_bound_takes_the_tightest_ceiling():
+    """A host line's PCIe bound (bench.pcie_bound): no faster than its host ->
+    device bytes at the H2D ceiling, its device -> host bytes at the D2H
+    ceiling, or both at the two directions' aggregate."""
+    c = {"h2d": 50.0, "d2h": 40.0, "both": 60.0}
+    assert abs(bench.pcie_bound(c, 16, 16) - 60e9 / 32) < 1  # symmetric: the aggregate
+    assert abs(bench.pcie_bound(c, 16, 0) - 50e9 / 16) < 1  # one way: that direction
+    assert abs(bench.pcie_bound(c, 4, 16) - 40e9 / 16) < 1  # mostly back: D2H
+    assert abs(bench.pcie_bound(c, 16, 8) - 60e9 / 24) < 1  # UID parts: 16 in, 8 out
 
 
 def test_compact_line_trims_to_the_cap_whatever_the_detail():

@@ -67,6 +67,9 @@ def test_seam_program_put_and_probed_get():
     # the same puts in the GPU's window order: every tab file equal to the batch-order store's
     assert r["win_order_same_tab_files"] >= 256 and r["win_order_found"] == r["ref_found"]
     assert r["win_range_put"] == r["n_put"]  # four window ranges, one handle each, put every key
+    # 8-B UID parts through shf_use_uid_parts: the store and every shf_uid as with the full hashes
+    assert r["parts_same_uids"] == r["n_put"] and r["parts_same_tab_files"] >= 256
+    assert r["parts_ref_found"] == r["parts_get_found"] == r["n_put"]
 
 
 @pytest.mark.gpu
@@ -129,6 +132,7 @@ def test_cpp_seam_program_own_hash_block_and_put_batch():
     p = subprocess.run([BIN_CPP, "100000"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     r = json.loads(p.stdout.strip().splitlines()[-1])
-    assert r["failures"] == 0 and r["checks"] == 4 * 9 + 6
+    assert r["failures"] == 0 and r["checks"] == 4 * 9 + 7
     assert r["found"] == r["right"] == r["n_put"] == 100000 and r["absent_found"] == 0
     assert r["fixed_found"] == 50000
+    assert r["parts_found"] == 50000  # UID parts through UseUidParts (include/shf_hash_batch_shf.hpp)

@@ -395,3 +395,60 @@ def test_host_keys_larger_than_the_stage(hb, dev, oracle, monkeypatch):
     assert np.array_equal(hb.hash_fixed_host(flat, big), oracle.hash_fixed(flat, big))
     off = np.array([0, 10, 10 + 3 * big - 100, 3 * big - 50, 3 * big], dtype=np.uint64)
     assert np.array_equal(hb.hash_var_host(flat, off), oracle.hash_var(flat, off))
+
+
+def test_eight_shards_share_the_copy_workers(hb, dev, oracle, monkeypatch):
+    """What an 8-GPU host caller hits: shf_hash_batch_*_multi
+    with n_devices = 8 from pageable buffers -- 8 shard threads whose chunks'
+    copy-outs (drain_async pieces that wait on each slot's event) share the one
+    pool of <= 12 copy workers with the staging copies -- here on one GPU
+    (SHF_HB_MULTI_SHARE_DEVICES). configs[4]'s 16-B keys at 100M and configs[3]'s
+    U[8,512] B at 10M: every key against the device kernels, a sample against
+    the oracle, and each call within a stated wall time (10 s; an unshared run
+    takes well under 1 s, so only a stall of the shared workers reaches it)."""
+    import time
+
+    from sharedhashfile_amd.keygen import device_random_bytes
+
+    monkeypatch.setenv("SHF_HB_MULTI_SHARE_DEVICES", "1")
+    limit_s = 10.0
+    n = 100_000_000
+    keys = device_random_bytes(n * 16, 401, dev)
+    ref = hb.hash_fixed(keys, 16)
+    host = keys.cpu().numpy()
+    del keys
+    times = []
+    for _ in range(2):  # the second call finds the workers and slots made
+        t0 = time.perf_counter()
+        got = hb.hash_fixed_host(host, 16, n_devices=8)
+        times.append(time.perf_counter() - t0)
+    assert torch.equal(torch.from_numpy(got.view(np.int64)).to(dev), ref)
+    del ref
+    idx = np.unique(np.concatenate([np.random.default_rng(401).integers(0, n, size=20000), [0, n - 1]]))
+    assert np.array_equal(got[idx], oracle.hash_fixed(host.reshape(n, 16)[idx], 16))
+    del got, host
+    m = 10_000_000
+    g = torch.Generator(device=dev)
+    g.manual_seed(402)
+    lens = torch.randint(8, 513, (m,), generator=g, device=dev, dtype=torch.int64)
+    off = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=off[1:])
+    del lens
+    data = device_random_bytes(int(off[-1].item()), 403, dev)
+    vref = hb.hash_var(data, off)
+    h_data, h_off = data.cpu().numpy(), off.cpu().numpy().view(np.uint64)
+    del data, off
+    vtimes = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        vgot = hb.hash_var_host(h_data, h_off, n_devices=8)
+        vtimes.append(time.perf_counter() - t0)
+    assert torch.equal(torch.from_numpy(vgot.view(np.int64)).to(dev), vref)
+    vidx = np.unique(np.random.default_rng(402).integers(0, m, size=2000))
+    sub_off = np.zeros(len(vidx) + 1, dtype=np.uint64)
+    sub_off[1:] = np.cumsum(h_off[vidx + 1] - h_off[vidx])
+    sub = np.concatenate([h_data[h_off[i]:h_off[i + 1]] for i in vidx])
+    assert np.array_equal(vgot[vidx], oracle.hash_var(sub, sub_off))
+    print("8 shards on one GPU: 100M x 16 B %s s (%.2f G keys/s), 10M x U[8,512] B %s s (%.3f G keys/s)" % (
+        ["%.3f" % t for t in times], n / min(times) / 1e9, ["%.3f" % t for t in vtimes], m / min(vtimes) / 1e9))
+    assert max(times) < limit_s and max(vtimes) < limit_s, (times, vtimes)
