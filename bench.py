@@ -44,6 +44,7 @@ distinct GPUs actually used.
 """
 import argparse
 import csv
+import ctypes
 import glob
 import json
 import os
@@ -861,12 +862,19 @@ PCIE_MB = 160  # bytes per direction of the PCIe ceiling copies (VERDICT r5 item
 
 def pcie_ceilings(dev, mb=PCIE_MB, reps=5):
     """The PCIe ceiling of this box, measured in the same run as the host lines
-    it bounds: hipMemcpyAsync (torch copy_, non_blocking) of `mb` MB between
-    page-locked host memory and HBM, host -> device alone, device -> host alone,
-    and both at once on two streams (each direction timed by HIP events on its
-    own stream), plus the HIP runtime's own pageable host -> device copy (the
+    it bounds, by the two mechanisms the host pipelines use:
+      * the copy engines: hipMemcpyAsync (torch copy_, non_blocking) of `mb` MB
+        between page-locked host memory and HBM, host -> device alone (h2d),
+        device -> host alone (d2h), and both at once on two streams (both: the
+        two directions' bytes over the later finish; both_h2d / both_d2h: each
+        direction timed by HIP events on its own stream);
+      * a kernel over PCIe (zero copy): the bench library's 16-B copy kernel
+        (SHF_HB_CEIL_COPY, k_fixed16's access shape) reading page-locked host
+        memory into HBM (zc_h2d), HBM into host memory (zc_d2h), and host into
+        host (zc_both: `mb` MB each way at once);
+    plus the HIP runtime's own pageable host -> device copy (h2d_pageable: the
     path pageable fixed-length keys take). GB/s (1e9 B/s), median of `reps`
-    after one untimed copy of each."""
+    after one untimed run of each."""
     import torch
 
     nb = mb * 1_000_000
@@ -893,7 +901,30 @@ def pcie_ceilings(dev, mb=PCIE_MB, reps=5):
         runs = [one(copies) for _ in range(reps)]
         return [float(np.median([r[i] for r in runs])) for i in range(len(copies))]
 
+    from sharedhashfile_amd import bench_ceiling as bc
+
+    zc_src, zc_dst = bc.host_device_ptr(h_src.data_ptr()), bc.host_device_ptr(h_dst.data_ptr())
+    copy_fn = bc.load().shf_hb_ceiling_async
+
+    def zc(src, dst):  # ms of one 16-B-per-lane copy kernel, nb bytes read and nb written
+        st = torch.cuda.current_stream(dev)
+        ts = []
+        for r in range(reps + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            a.record(st)
+            rc = copy_fn(bc.CEIL_COPY, ctypes.c_void_p(src), nb, None, ctypes.c_void_p(dst), nb // 16,
+                         ctypes.c_void_p(st.cuda_stream))
+            b.record(st)
+            torch.cuda.synchronize(dev)
+            if rc:
+                raise RuntimeError("shf_hb_ceiling_async over PCIe: %d" % rc)
+            if r:
+                ts.append(a.elapsed_time(b))
+        return float(np.median(ts))
+
     gbs = lambda ms: nb / (ms * 1e-3) / 1e9  # noqa: E731
+    zc_h2d, zc_d2h, zc_both = zc(zc_src, d_a.data_ptr()), zc(d_b.data_ptr(), zc_dst), zc(zc_src, zc_dst)
     h2d, = med([(s1, d_a, h_src)])
     d2h, = med([(s2, h_dst, d_b)])
     both_h2d, both_d2h = med([(s1, d_a, h_src), (s2, h_dst, d_b)])
@@ -908,16 +939,24 @@ def pcie_ceilings(dev, mb=PCIE_MB, reps=5):
             "both_h2d": round(gbs(both_h2d), 2), "both_d2h": round(gbs(both_d2h), 2),
             "both": round(2 * nb / (max(both_h2d, both_d2h) * 1e-3) / 1e9, 2),
             "h2d_pageable": round(nb / float(np.median(pg[1:])) / 1e9, 2),
+            "zc_h2d": round(gbs(zc_h2d), 2), "zc_d2h": round(gbs(zc_d2h), 2), "zc_both": round(2 * gbs(zc_both), 2),
             "bytes_per_copy": nb}
 
 
 def pcie_bound(ceil, bytes_in, bytes_out):
     """Keys/s the PCIe ceilings allow a line moving bytes_in host -> device and
-    bytes_out device -> host per key: no faster than either direction alone,
-    nor than both directions' aggregate when they run at once."""
-    t = max(bytes_in / (ceil["h2d"] * 1e9), bytes_out / (ceil["d2h"] * 1e9),
-            (bytes_in + bytes_out) / (ceil["both"] * 1e9))
-    return 1.0 / t
+    bytes_out device -> host per key, by the better of the two mechanisms
+    (copy engines, or a kernel over PCIe: keys "zc_*"): through one, no faster
+    than either direction alone, nor than both directions' aggregate when they
+    run at once."""
+    best = 0.0
+    for pre in ("", "zc_"):
+        if pre + "h2d" not in ceil:
+            continue
+        t = max(bytes_in / (ceil[pre + "h2d"] * 1e9), bytes_out / (ceil[pre + "d2h"] * 1e9),
+                (bytes_in + bytes_out) / (ceil[pre + "both"] * 1e9))
+        best = max(best, 1.0 / t)
+    return best
 
 
 def time_host_inclusive(args, dev):
@@ -1539,7 +1578,8 @@ def compact_line(full, detail_path):
                                   if isinstance(v, dict) and "value" in v}
         if isinstance(hi.get("ceilings_gbs"), dict):
             c = hi["ceilings_gbs"]
-            line["host_inclusive"]["pcie_gbs"] = {k: c[k] for k in ("h2d", "d2h", "both", "h2d_pageable") if k in c}
+            line["host_inclusive"]["pcie_gbs"] = {k: c[k] for k in ("h2d", "d2h", "both", "h2d_pageable", "zc_h2d",
+                                                                    "zc_d2h", "zc_both") if k in c}
         line["host_inclusive"]["verified"] = hi.get("verified")
     sec, ceil = {}, {}
     for name, s in (full.get("secondary") or {}).items():

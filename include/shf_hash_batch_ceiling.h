@@ -48,6 +48,10 @@ extern "C" {
 SHF_HB_API int shf_hb_ceiling_async(int kind, const void *d_src, uint64_t src_bytes, const uint32_t *d_idx,
                                     void *d_dst, uint64_t n, void *hip_stream);
 
+/* *dev = the device address of page-locked host memory (hipHostGetDevicePointer), so that a ceiling kernel
+ * can read or write host memory over PCIe as the product's zero copy does; SHF_HB_ERR_ARG if not mappable. */
+SHF_HB_API int shf_hb_host_device_ptr(const void *host, void **dev);
+
 #ifdef __cplusplus
 }
 #endif

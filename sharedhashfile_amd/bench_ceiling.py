@@ -43,5 +43,16 @@ def load():
     v = ctypes.c_void_p
     lib.shf_hb_ceiling_async.argtypes = [ctypes.c_int, v, ctypes.c_uint64, v, v, ctypes.c_uint64, v]
     lib.shf_hb_ceiling_async.restype = ctypes.c_int
+    lib.shf_hb_host_device_ptr.argtypes = [v, ctypes.POINTER(v)]
+    lib.shf_hb_host_device_ptr.restype = ctypes.c_int
     _lib = lib
     return lib
+
+
+def host_device_ptr(host_ptr):
+    """Device address (int) of page-locked host memory at host_ptr."""
+    d = ctypes.c_void_p()
+    rc = load().shf_hb_host_device_ptr(ctypes.c_void_p(host_ptr), ctypes.byref(d))
+    if rc:
+        raise RuntimeError("shf_hb_host_device_ptr: %d" % rc)
+    return d.value

@@ -258,3 +258,16 @@ extern "C" int shf_hb_ceiling_async(int kind, const void* d_src, uint64_t src_by
   }
   return hipGetLastError() == hipSuccess ? SHF_HB_OK : SHF_HB_ERR_HIP;
 }
+
+// The device address of page-locked host memory (bench.py pcie_ceilings: the
+// copy kernel run over PCIe, reading and/or writing host memory as the
+// product's zero copy does); SHF_HB_ERR_ARG for memory the device cannot map.
+extern "C" int shf_hb_host_device_ptr(const void* host, void** dev) {
+  if (!host || !dev) return SHF_HB_ERR_ARG;
+  *dev = nullptr;
+  if (hipHostGetDevicePointer(dev, const_cast<void*>(host), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return SHF_HB_ERR_ARG;
+  }
+  return SHF_HB_OK;
+}

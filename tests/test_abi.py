@@ -45,13 +45,14 @@ def test_bench_library_is_separate():
     from sharedhashfile_amd import bench_ceiling
 
     ceiling = hbmod.header_functions(os.path.join(ROOT, "include", "shf_hash_batch_ceiling.h"))
-    assert ceiling == ["shf_hb_ceiling_async"]
+    assert ceiling == ["shf_hb_ceiling_async", "shf_hb_host_device_ptr"]
     hbmod.load()
     out = subprocess.check_output(["nm", "-D", "--defined-only", bench_ceiling.BENCH_LIB_PATH]).decode()
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     assert exported == set(ceiling), exported
     assert bench_ceiling.load().shf_hb_ceiling_async(0, None, 0, None, None, 0, None) == hbmod.OK  # n == 0
     assert bench_ceiling.load().shf_hb_ceiling_async(99, 16, 16, None, 16, 1, None) == hbmod.ERR_ARG
+    assert bench_ceiling.load().shf_hb_host_device_ptr(None, None) == hbmod.ERR_ARG
 
 
 def test_header_compiles_as_c():

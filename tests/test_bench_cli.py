@@ -252,6 +252,11 @@ def test_pcie_bound_takes_the_tightest_ceiling():
     assert abs(bench.pcie_bound(c, 16, 0) - 50e9 / 16) < 1  # one way: that direction
     assert abs(bench.pcie_bound(c, 4, 16) - 40e9 / 16) < 1  # mostly back: D2H
     assert abs(bench.pcie_bound(c, 16, 8) - 60e9 / 24) < 1  # UID parts: 16 in, 8 out
+    # a kernel over PCIe (zero copy) moving both directions at once: the better mechanism wins
+    z = dict(c, zc_h2d=52.0, zc_d2h=45.0, zc_both=84.0)
+    assert abs(bench.pcie_bound(z, 16, 16) - 84e9 / 32) < 1
+    assert abs(bench.pcie_bound(z, 16, 0) - 52e9 / 16) < 1
+    assert abs(bench.pcie_bound(z, 4, 16) - 45e9 / 16) < 1
 
 
 def test_compact_line_trims_to_the_cap_whatever_the_detail():
