@@ -168,6 +168,11 @@ SHF_HB_API int shf_hash_batch_fixed_multi(const void *keys, uint32_t key_len, ui
                                shf_hash128 *out, int n_devices);
 SHF_HB_API int shf_hash_batch_var_multi(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
                              shf_hash128 *out, int n_devices);
+/* The same with 8-B UID parts out instead of 16-B records (see "UID parts"). */
+SHF_HB_API int shf_uid_parts_batch_fixed_multi(const void *keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                               uint64_t *parts, int n_devices);
+SHF_HB_API int shf_uid_parts_batch_var_multi(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
+                                             uint64_t *parts, int n_devices);
 
 /* ---- kernel selection (tests and benchmarks) ------------------------------- */
 #define SHF_HB_KERNEL_AUTO 0    /* what every function above uses */

@@ -74,6 +74,8 @@ _SIGS = {
     "shf_hash_batch_var_async": [_VP, _VP, _U64, _U32, _VP, _VP],
     "shf_uid_parts_batch_fixed": [_VP, _U32, _U64, _U32, _VP, _INT],
     "shf_uid_parts_batch_var": [_VP, _VP, _U64, _U32, _VP, _INT],
+    "shf_uid_parts_batch_fixed_multi": [_VP, _U32, _U64, _U32, _VP, _INT],
+    "shf_uid_parts_batch_var_multi": [_VP, _VP, _U64, _U32, _VP, _INT],
     "shf_uid_parts_batch_fixed_async": [_VP, _U32, _U64, _U32, _VP, _VP],
     "shf_uid_parts_batch_var_async": [_VP, _VP, _U64, _U32, _VP, _VP],
     "shf_hash_batch_fixed_multi": [_VP, _U32, _U64, _U32, _VP, _INT],
@@ -694,28 +696,38 @@ def hash_fixed_host(keys, key_len=None, seed=SEED, n_devices=None):
     return out
 
 
-def uid_parts_fixed_host(keys, key_len=None, seed=SEED):
+def uid_parts_fixed_host(keys, key_len=None, seed=SEED, n_devices=None):
     """Host keys in, host uint64[n] UID parts out (shf_uid_parts_batch_fixed,
-    SHF_HASH_MEM_HOST: 8 B per key back instead of 16)."""
+    SHF_HASH_MEM_HOST: 8 B per key back instead of 16). n_devices: None = the
+    current device only, else shf_uid_parts_batch_fixed_multi."""
     keys = _np_u8(keys)
     if key_len is None:
         n, key_len = keys.shape
     else:
         n = keys.size // key_len if key_len else 0
     out = np.empty(n, dtype=np.uint64)
-    _check(load().shf_uid_parts_batch_fixed(keys.ctypes.data, key_len, n, seed, out.ctypes.data, MEM_HOST),
-           "shf_uid_parts_batch_fixed")
+    if n_devices is None:
+        _check(load().shf_uid_parts_batch_fixed(keys.ctypes.data, key_len, n, seed, out.ctypes.data, MEM_HOST),
+               "shf_uid_parts_batch_fixed")
+    else:
+        _check(load().shf_uid_parts_batch_fixed_multi(keys.ctypes.data, key_len, n, seed, out.ctypes.data,
+                                                      n_devices), "shf_uid_parts_batch_fixed_multi")
     return out
 
 
-def uid_parts_var_host(data, offsets, seed=SEED):
-    """Variable-length host keys in, host uint64[n] UID parts out (shf_uid_parts_batch_var, SHF_HASH_MEM_HOST)."""
+def uid_parts_var_host(data, offsets, seed=SEED, n_devices=None):
+    """Variable-length host keys in, host uint64[n] UID parts out (shf_uid_parts_batch_var, SHF_HASH_MEM_HOST;
+    n_devices as uid_parts_fixed_host)."""
     data = _np_u8(data)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = max(offsets.size - 1, 0)
     out = np.empty(n, dtype=np.uint64)
-    _check(load().shf_uid_parts_batch_var(data.ctypes.data, offsets.ctypes.data, n, seed, out.ctypes.data, MEM_HOST),
-           "shf_uid_parts_batch_var")
+    if n_devices is None:
+        _check(load().shf_uid_parts_batch_var(data.ctypes.data, offsets.ctypes.data, n, seed, out.ctypes.data,
+                                              MEM_HOST), "shf_uid_parts_batch_var")
+    else:
+        _check(load().shf_uid_parts_batch_var_multi(data.ctypes.data, offsets.ctypes.data, n, seed, out.ctypes.data,
+                                                    n_devices), "shf_uid_parts_batch_var_multi")
     return out
 
 

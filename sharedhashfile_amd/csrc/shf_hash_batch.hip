@@ -1427,6 +1427,30 @@ int shf_hash_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_
   });
 }
 
+int shf_uid_parts_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, uint64_t* parts,
+                                    int n_devices) {
+  HB_ENTER();
+  if (n == 0) return SHF_HB_OK;
+  if (!parts || (!keys && key_len) || key_len > kMaxKeyLen) return SHF_HB_ERR_ARG;
+  const uint8_t* k = (const uint8_t*)keys;
+  return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
+    return host_fixed(k ? k + lo * key_len : nullptr, key_len, hi - lo, seed, uid_job(parts + lo));
+  });
+}
+
+int shf_uid_parts_batch_var_multi(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed,
+                                  uint64_t* parts, int n_devices) {
+  HB_ENTER();
+  if (n == 0) return SHF_HB_OK;
+  if (!parts || !offsets || !bytes) return SHF_HB_ERR_ARG;
+  int rc = check_var_lengths_host(offsets, n);
+  if (rc) return rc;
+  const uint8_t* b = (const uint8_t*)bytes;
+  return run_multi(n, n_devices, [&](uint64_t lo, uint64_t hi) {
+    return host_var(b, offsets + lo, hi - lo, seed, uid_job(parts + lo));
+  });
+}
+
 int shf_row_index_create(uint64_t n_slots, shf_row_index** out) {
   HB_ENTER();
   if (!out) return SHF_HB_ERR_ARG;

@@ -178,3 +178,24 @@ def test_host_uid_config4_1b_16b(hb, dev, oracle):
     del ref
     idx = np.unique(np.concatenate([np.random.default_rng(323).integers(0, n, size=20000), [0, n - 1]]))
     assert np.array_equal(got[idx], _want_fixed(oracle, host.reshape(n, 16)[idx], 16))
+
+
+@pytest.mark.parametrize("n_devices", [0, 3, 8])
+def test_host_uid_multi(hb, dev, oracle, monkeypatch, n_devices):
+    """shf_uid_parts_batch_{fixed,var}_multi: the host batch split over shard
+    threads (here sharing this GPU: SHF_HB_MULTI_SHARE_DEVICES; 0 = every
+    visible device), every key's parts as one call makes them."""
+    monkeypatch.setenv("SHF_HB_MULTI_SHARE_DEVICES", "1")
+    n = 3_000_017
+    flat = np.frombuffer(splitmix_bytes(n * 16, 330 + n_devices), dtype=np.uint8)
+    assert np.array_equal(hb.uid_parts_fixed_host(flat, 16, n_devices=n_devices), _want_fixed(oracle, flat, 16))
+    rng = np.random.default_rng(331 + n_devices)
+    m = 200_003
+    lens = rng.integers(0, 600, size=m)
+    off = np.zeros(m + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    assert np.array_equal(hb.uid_parts_var_host(data, off, n_devices=n_devices),
+                          oracle.uid_parts(oracle.hash_var(data, off)))
+    assert np.array_equal(hb.uid_parts_fixed_host(flat[:48], 16, n_devices=n_devices),
+                          _want_fixed(oracle, flat[:48], 16))  # fewer keys than shards
