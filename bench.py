@@ -1573,7 +1573,7 @@ def compact_line(full, detail_path):
     cpu = full.get("cpu_baseline")
     if cpu:
         c = {"value": _sig(cpu["value"], 5), "unit": cpu["unit"], "cores": cpu["cores"], "kind": cpu["kind"],
-             "sample": cpu["sample"][:160]}
+             "sample": cpu["sample"][:120]}
         mt = next((v for k, v in cpu.items() if k.startswith("threads")), None)
         if mt:
             c["multi"] = {"value": _sig(mt["value"], 5), "cores": mt["cores"]}
@@ -1595,8 +1595,10 @@ def compact_line(full, detail_path):
         if name.startswith("ceil_"):
             ceil[name] = r["achieved"] if r.get("unit") == "GB/s" else _sig(s["value"], 4)
             continue
-        e = {"value": _sig(s["value"], 5), "unit": s["unit"], "kernel_us": _sig(r.get("kernel_us"), 5),
+        e = {"value": _sig(s["value"], 5), "kernel_us": _sig(r.get("kernel_us"), 5),
              "frac": r.get("frac"), "frac_of_ceiling": r.get("frac_of_copy_ceiling")}
+        if s["unit"] != full["unit"]:  # a secondary line's unit only where it is not the line's own (keys/s)
+            e["unit"] = s["unit"]
         if r.get("traffic_over_algorithmic") is not None:
             e["traffic_x"] = r["traffic_over_algorithmic"]
         for k in ("frac_per_key", "frac_of_ceiling_unique"):

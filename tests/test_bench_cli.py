@@ -283,3 +283,23 @@ def test_shared_order_kernels_go_to_the_workload_that_ran_them():
     vals = bench.parse_pmc_rows(rows, {"winorder": g, "hashwin16": g})
     assert bench.pmc_medians(vals["winorder"])["FETCH_SIZE"] == 100.0 + 1.0 + 10.0
     assert bench.pmc_medians(vals["hashwin16"])["FETCH_SIZE"] == 100.0 + 7.0 + 70.0
+
+
+def test_a_real_run_record_leaves_room_under_the_cap():
+    """The full record of a real N = 1 run on the box (round 6, with the host
+    lines' PCIe fields): its stdout line keeps every block and at least 200 B
+    under the 4-KB cap, so digits that differ by run cannot push a block out."""
+    import os
+
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r6", "bench_r6f",
+                     "bench_detail_n1.json")
+    if not os.path.exists(p):  # profiles/ does not travel to the GPU box
+        pytest.skip("profiles/r6/bench_r6f absent")
+    full = bench.json.load(open(p))
+    line = bench.compact_line(full, "gpurun_out/bench_detail_n1.json")
+    s = bench.json.dumps(line)
+    assert len(s) <= bench.LINE_MAX_BYTES - 200, len(s)
+    for k in ("host_inclusive", "secondary", "ceilings_gbs", "cpu_baseline", "roofline"):
+        assert k in line, k
+    assert set(line["secondary"]) == set(full["secondary"]) - {k for k in full["secondary"] if k.startswith("ceil_")}
+    assert line["host_inclusive"]["uid16_pageable"][1] == full["host_inclusive"]["uid16_pageable"]["frac_of_pcie"]
