@@ -20,7 +20,8 @@
  *   7. 8-B UID parts (shf_uid_parts_batch_var, host memory) through
  *      shf_use_uid_parts: a store put from parts is byte-equal to one put from
  *      the full hashes, with the same shf_uid per key, and the reference's
- *      own get finds every key in it.
+ *      own get finds every key in it; gets and dels with the parts in the seam
+ *      give the reference's answers.
  *
  * TEST INFRASTRUCTURE: built by tests/c/Makefile where /root/reference exists
  * (the reference's headers are needed to compile it), into tests/c/build/, which
@@ -306,6 +307,25 @@ int main(int argc, char **argv)
         }
     }
     if (pgot != n_put || pgot_any != n_put) return fail("uid parts: get through shf_use_uid_parts");
+    /* del through the parts (shf_del_key_val finds the key with the same bits): every even key gone,
+     * every odd one still found by the reference's own get; deleting an absent key finds nothing */
+    uint64_t pdel = 0, pdel_absent = 0;
+    for (uint64_t i = 0; i < n; i += 2) {
+        shf_use_uid_parts(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), parts[i]);
+        const uint32_t r = shf_del_key_val(pshf);
+        if (i < n_put) pdel += r == SHF_RET_KEY_FOUND;
+        else pdel_absent += r == SHF_RET_KEY_FOUND;
+    }
+    uint64_t pleft = 0, pleft_right = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        shf_make_hash(bytes + off[i], (uint32_t)(off[i + 1] - off[i]));
+        if (shf_get_key_val_copy(pshf) == SHF_RET_KEY_FOUND) {
+            ++pleft;
+            pleft_right += (i & 1) && i < n_put && memcmp(shf_val, &i, 8) == 0;
+        }
+    }
+    if (pdel != (n_put + 1) / 2 || pdel_absent != 0 || pleft != n_put / 2 || pleft_right != n_put / 2)
+        return fail("uid parts: del through shf_use_uid_parts");
     /* fixed 16-byte keys: the parts of the fixed-length entry point */
     uint64_t *fparts = malloc(nf * sizeof *fparts);
     if (shf_uid_parts_batch_fixed(fk, 16, nf, SHF_HASH_BATCH_SEED, fparts, SHF_HASH_MEM_HOST) != SHF_HB_OK)
@@ -318,12 +338,14 @@ int main(int argc, char **argv)
     printf("{\"n_put\": %llu, \"n_query\": %llu, \"ref_found\": %llu, \"ref_right\": %llu, \"probed_found\": %llu, "
            "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu, \"win_order_same_tab_files\": %lld, "
            "\"win_order_found\": %llu, \"win_range_put\": %lld, \"parts_same_uids\": %llu, "
-           "\"parts_same_tab_files\": %lld, \"parts_ref_found\": %llu, \"parts_get_found\": %llu}\n",
+           "\"parts_same_tab_files\": %lld, \"parts_ref_found\": %llu, \"parts_get_found\": %llu, "
+           "\"parts_deleted\": %llu, \"parts_left\": %llu}\n",
            (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
            (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
            (unsigned long long)ffound, (long long)same_files, (unsigned long long)wfound2,
            (long long)range_put, (unsigned long long)uid_same, (long long)parts_same_files,
-           (unsigned long long)pright, (unsigned long long)pgot);
+           (unsigned long long)pright, (unsigned long long)pgot, (unsigned long long)pdel,
+           (unsigned long long)pleft);
     shf_detach(wshf);
     /* the stores' files go with the folder (shf_del would run `du` and `rm` through popen) */
     shf_detach(shf);

@@ -70,6 +70,7 @@ def test_seam_program_put_and_probed_get():
     # 8-B UID parts through shf_use_uid_parts: the store and every shf_uid as with the full hashes
     assert r["parts_same_uids"] == r["n_put"] and r["parts_same_tab_files"] >= 256
     assert r["parts_ref_found"] == r["parts_get_found"] == r["n_put"]
+    assert r["parts_deleted"] == r["parts_left"] == r["n_put"] // 2  # del through the parts, then the CPU get
 
 
 @pytest.mark.gpu
