@@ -199,3 +199,28 @@ def test_host_uid_multi(hb, dev, oracle, monkeypatch, n_devices):
                           oracle.uid_parts(oracle.hash_var(data, off)))
     assert np.array_equal(hb.uid_parts_fixed_host(flat[:48], 16, n_devices=n_devices),
                           _want_fixed(oracle, flat[:48], 16))  # fewer keys than shards
+
+
+def test_host_uid_mixed_and_unaligned_buffers(hb, dev, oracle, monkeypatch):
+    """Pageable keys with a page-locked parts output (the kernel stores the
+    parts straight into it) and the reverse; a parts output 4 B off 8-B
+    alignment in both kinds of memory; a fixed key longer than a staging slot."""
+    lib = hb.load()
+    n = 1_000_003
+    flat = np.frombuffer(splitmix_bytes(n * 16 + 16, 340), dtype=np.uint8)[: n * 16]
+    want = _want_fixed(oracle, flat, 16)
+    pk = torch.from_numpy(flat.copy()).pin_memory()
+    for keys_ptr in (flat.ctypes.data, pk.data_ptr()):
+        pout = torch.zeros(2 * n + 2, dtype=torch.int32).pin_memory()  # 4-B steps: room for a misaligned start
+        host = np.zeros(2 * n + 2, dtype=np.uint32)
+        for base, arr in ((pout.data_ptr(), pout.numpy()), (host.ctypes.data, host)):
+            for skew in (0, 4):
+                arr[:] = 0
+                rc = lib.shf_uid_parts_batch_fixed(keys_ptr, 16, n, 12345, base + skew, hb.MEM_HOST)
+                assert rc == 0
+                got = np.frombuffer(arr.view(np.uint8)[skew:skew + 8 * n].tobytes(), dtype=np.uint64)
+                assert np.array_equal(got, want), (keys_ptr == pk.data_ptr(), base == host.ctypes.data, skew)
+    monkeypatch.setenv("SHF_HB_STAGE_MB", "1")
+    big = (1 << 20) + 4099  # longer than a 1-MiB slot: one key at a time through a device buffer of its own
+    kb = np.frombuffer(splitmix_bytes(3 * big, 341), dtype=np.uint8)
+    assert np.array_equal(hb.uid_parts_fixed_host(kb, big), _want_fixed(oracle, kb, big))
