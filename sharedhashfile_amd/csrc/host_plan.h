@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -303,9 +304,10 @@ struct Ticket {
 };
 
 // Worker threads for the staging copies, shared by every calling thread: a
-// worker is started when a batch has more pieces than there are workers, and
-// parks on the queue between batches (the library keeps one pool for the
-// process's life). submit() returns at once with a Ticket; run() runs
+// worker is started when a batch has more pieces than there are workers, parks
+// on the queue between batches and ends after `idle` without a piece (the
+// library keeps one pool for the process's life; its workers live only while
+// the process hashes). submit() returns at once with a Ticket; run() runs
 // pieces[0] on the caller and returns when every piece has run.
 //
 // fork(): a child has only the forking thread, so the parent's workers do not
@@ -320,7 +322,10 @@ struct Ticket {
 // workers, /root/reference/src/test.f.shf.c:274-336).
 class CopyPool {
  public:
-  explicit CopyPool(size_t max_workers = (size_t)-1) : max_workers_(max_workers) {}
+  // idle: a worker that finds no piece for this long ends (a later batch starts
+  // workers again), so a process that stops hashing keeps no copy threads.
+  explicit CopyPool(size_t max_workers = (size_t)-1, std::chrono::milliseconds idle = std::chrono::seconds(10))
+      : max_workers_(max_workers), idle_(idle) {}
 
   std::shared_ptr<Ticket> submit(std::vector<std::function<int()>> pieces) {
     auto t = std::make_shared<Ticket>();
@@ -416,7 +421,15 @@ class CopyPool {
       std::function<void()> f;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return !q_.empty(); });
+        // (a system_clock deadline: libstdc++ waits on it with pthread_cond_timedwait, which
+        // ThreadSanitizer follows; a steady_clock wait_for uses pthread_cond_clockwait, which
+        // gcc 11's TSan does not intercept -- it then reports false double locks)
+        if (!cv_.wait_until(lk, std::chrono::system_clock::now() + idle_, [&] { return !q_.empty(); })) {
+          // idle: end this worker (the count drops under the lock, so a batch queued
+          // from now on starts a worker of its own; one queued before was seen above)
+          --workers_;
+          return;
+        }
         f = std::move(q_.front());
         q_.pop_front();
       }
@@ -428,6 +441,7 @@ class CopyPool {
   std::deque<std::function<void()>> q_;
   size_t workers_ = 0;
   const size_t max_workers_;
+  const std::chrono::milliseconds idle_;
   bool forked_ = false;
 };
 
