@@ -396,10 +396,11 @@ size_t copy_threads() {
   return v >= 1 && v <= 64 ? (size_t)v : 12;
 }
 
-// Persistent staging-copy workers shared by every calling thread (host_plan.h
-// CopyPool): started on first use (up to SHF_HB_COPY_THREADS - 1), never per
-// chunk. Deliberately never destroyed: the workers park on the queue and end
-// with the process.
+// Staging-copy workers shared by every calling thread (host_plan.h CopyPool):
+// started on first use (up to SHF_HB_COPY_THREADS - 1), never per chunk; a
+// worker that finds no piece for 10 s ends, and the next batch starts workers
+// again. The pool object itself is deliberately never destroyed (a worker may
+// still be returning from it at process exit).
 using shfhb::plan::CopyPool;
 using shfhb::plan::Ticket;
 
