@@ -754,9 +754,10 @@ int host_fixed_big(int dev, const uint8_t* keys, uint32_t key_len, uint64_t n, u
 
 // Zero copy: page-locked caller buffers that the device can address are read
 // and written by the hashing kernel itself over PCIe. The copy engines run one
-// direction at a time (H2D 57 GB/s, D2H 57 GB/s, both at once 28-48 GB/s each,
-// tools/host_zero_copy_probe.py), while a kernel's loads and stores use both
-// directions together. 160 MB of keys, G keys/s zero copy vs staged
+// direction at a time (bench.py pcie_ceilings, same run as the host lines:
+// H2D 57, D2H 57, both at once on two streams 57 GB/s together), while a
+// kernel's loads and stores use both directions together (a 16-B copy kernel
+// over PCIe: 81 GB/s together). 160 MB of keys, G keys/s zero copy vs staged
 // (profiles/r2/host_zero_copy/): 16 B 2.54 vs 1.74, 32 B 1.55 vs 1.11,
 // 48 B 1.01 vs 0.81, 64 B 0.79 vs 0.68, 128 B 0.38 vs 0.33. Used for keys up
 // to SHF_HB_ZERO_COPY_MAX_KEY bytes (default 128; 0 turns it off): past that
