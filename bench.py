@@ -1027,6 +1027,7 @@ def time_host_inclusive(args, dev):
     vpo = torch.empty((n, 2), dtype=torch.int64).pin_memory()
     uout = np.empty(n, dtype=np.uint64)
     upo = torch.empty(n, dtype=torch.int64).pin_memory()
+    perm = np.empty(n, dtype=np.uint32)
     cases = [
         ("fixed16_pageable", lambda: lib.shf_hash_batch_fixed(keys.ctypes.data, 16, n, SEED, out.ctypes.data,
                                                               hb.MEM_HOST), 5),
@@ -1050,9 +1051,17 @@ def time_host_inclusive(args, dev):
         ("uid16_pinned_staged", lambda: _staged(lambda: lib.shf_uid_parts_batch_fixed(pk.data_ptr(), 16, n, SEED,
                                                                                       upo.data_ptr(), hb.MEM_HOST)),
          5),
+        # hash (or UID parts) + window order in one call: the order (4 B/key) comes back too
+        # (shf_put_batch_var_win_ordered / _parts_win_ordered's GPU call)
+        ("hashwin16_pageable", lambda: lib.shf_hash_batch_fixed_win(keys.ctypes.data, 16, n, SEED, out.ctypes.data,
+                                                                    perm.ctypes.data, None, hb.MEM_HOST), 5),
+        ("uidwin16_pageable", lambda: lib.shf_uid_parts_batch_fixed_win(keys.ctypes.data, 16, n, SEED,
+                                                                        uout.ctypes.data, perm.ctypes.data, None,
+                                                                        hb.MEM_HOST), 5),
     ]
     mean_len = float(off[-1]) / n
-    wire = {"fixed16": (16, 16), "var": (mean_len + 8, 16), "uid16": (16, 8)}  # (host->device, device->host) B/key
+    wire = {"fixed16": (16, 16), "var": (mean_len + 8, 16), "uid16": (16, 8), "hashwin16": (16, 20),
+            "uidwin16": (16, 12)}  # (host->device, device->host) B/key
     for name, fn, reps in cases:
         # two untimed calls: the HIP runtime's first hipMemcpyAsync calls from a page-locked buffer it has not
         # copied from before take 7-14 ms to enqueue instead of 0.03 ms (SHF_HB_TRACE copy_in_ms, round 6:
@@ -1094,6 +1103,8 @@ def time_host_inclusive(args, dev):
         ok = ok and np.array_equal(vout[idx], vw) and np.array_equal(vpo.numpy().view(np.uint64)[idx], vw)
         uw = o.uid_parts(want)
         ok = ok and np.array_equal(uout[idx], uw) and np.array_equal(upo.numpy().view(np.uint64)[idx], uw)
+        # the window order of the last call (uidwin16): the stable order of every key's window byte
+        ok = ok and np.array_equal(perm, np.argsort((uout & np.uint64(0xFF)).astype(np.int64), kind="stable"))
         res["verified"] = bool(ok)
     except Exception as e:  # noqa: BLE001
         res["verified"] = None
@@ -1581,9 +1592,10 @@ def compact_line(full, detail_path):
     else:
         line["cpu_baseline"] = None
     hi = full.get("host_inclusive")
-    if hi:  # per line [keys/s, frac_of_pcie]; the PCIe ceilings (GB/s) of the same run
-        line["host_inclusive"] = {k: [_sig(v["value"], 4), v.get("frac_of_pcie")] for k, v in hi.items()
-                                  if isinstance(v, dict) and "value" in v}
+    if hi:  # per line [G keys/s, frac_of_pcie]; the PCIe ceilings (GB/s) of the same run
+        line["host_inclusive"] = {"unit": "G keys/s"}
+        line["host_inclusive"].update({k: [round(v["value"] / 1e9, 3), v.get("frac_of_pcie")] for k, v in hi.items()
+                                       if isinstance(v, dict) and "value" in v})
         if isinstance(hi.get("ceilings_gbs"), dict):
             c = hi["ceilings_gbs"]
             line["host_inclusive"]["pcie_gbs"] = {k: c[k] for k in ("h2d", "d2h", "both", "h2d_pageable", "zc_h2d",

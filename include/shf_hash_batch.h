@@ -401,6 +401,16 @@ SHF_HB_API int shf_hash_batch_fixed_win(const void *keys, uint32_t key_len, uint
                                         shf_hash128 *out, uint32_t *perm, uint32_t *win_start, int mem);
 SHF_HB_API int shf_hash_batch_var_win(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
                                       shf_hash128 *out, uint32_t *perm, uint32_t *win_start, int mem);
+/* UID parts + window order in one call: parts[] as shf_uid_parts_batch_fixed /
+ * _var, perm / win_start exactly as shf_win_order computes them from the
+ * batch's hashes (the window is SHF_UID_PARTS_WIN(parts[i]) = h1 & 0xff). With
+ * host memory 8 B of parts + 4 B of order per key cross PCIe back, instead of
+ * 16 + 4 (a window-ordered put from parts). mem, win_start
+ * and errors as shf_hash_batch_fixed_win / _var_win. */
+SHF_HB_API int shf_uid_parts_batch_fixed_win(const void *keys, uint32_t key_len, uint64_t n, uint32_t seed,
+                                             uint64_t *parts, uint32_t *perm, uint32_t *win_start, int mem);
+SHF_HB_API int shf_uid_parts_batch_var_win(const void *bytes, const uint64_t *offsets, uint64_t n, uint32_t seed,
+                                           uint64_t *parts, uint32_t *perm, uint32_t *win_start, int mem);
 /* The same with a forced hashing kernel (tests and benchmarks; SHF_HB_KERNEL_*). */
 SHF_HB_API int shf_hash_batch_fixed_win_kernel_async(const void *d_keys, uint32_t key_len, uint64_t n,
                                                      uint32_t seed, shf_hash128 *d_out, uint32_t *d_perm,

@@ -20,6 +20,8 @@
  *   shf_get_batch_probed()   INTEGRATION.md §6: a get batch driven by row
  *                            pre-probe records, falling back to the ordinary
  *                            get with the batch hash
+ *   shf_put_batch_var_parts_win_ordered()
+ *                            the window-ordered put from UID parts
  *   shf_put_batch_var_win_ordered(), shf_get_batch_win_ordered()
  *                            the same put / get loops run in
  *                            the GPU's window order (shf_win_order): the store
@@ -213,6 +215,41 @@ static inline int64_t shf_put_batch_var_win_ordered(SHF *shf, const char *bytes,
                 break;
         }
     free(h);
+    if (!perm_out) free(perm);
+    return rc == SHF_HB_OK ? (int64_t)j : rc;
+}
+
+/* shf_put_batch_var_win_ordered() with UID parts: one GPU call
+ * (shf_uid_parts_batch_var_win, host memory: 8 B of parts + 4 B of order per
+ * key cross PCIe back instead of 16 + 4), then shf_use_uid_parts() +
+ * shf_put_key_val() per key in window order; the store (files, uids) ends as
+ * shf_put_batch_var() leaves it. perm_out / uids_out (optional, n entries):
+ * the order used and shf_uid after each put (in batch index order). Returns as
+ * shf_put_batch_var_win_ordered(). */
+static inline int64_t shf_put_batch_var_parts_win_ordered(SHF *shf, const char *bytes, const uint64_t *offsets,
+                                                          uint64_t n, const char *vals, const uint64_t *val_offsets,
+                                                          uint32_t *perm_out, uint32_t *uids_out)
+{
+    if (n == 0) return 0;
+    uint64_t *parts = (uint64_t *)malloc(n * sizeof *parts);
+    uint32_t *perm = perm_out ? perm_out : (uint32_t *)malloc(n * sizeof *perm);
+    if (!parts || !perm) {
+        free(parts);
+        if (!perm_out) free(perm);
+        return SHF_HB_ERR_NOMEM;
+    }
+    int rc = shf_uid_parts_batch_var_win(bytes, offsets, n, SHF_HASH_BATCH_SEED, parts, perm, NULL, SHF_HASH_MEM_HOST);
+    uint64_t j = 0;
+    if (rc == SHF_HB_OK)
+        for (; j < n; ++j) {
+            const uint64_t i = perm[j];
+            shf_use_uid_parts(bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]), parts[i]);
+            if (shf_put_key_val(shf, vals + val_offsets[i], (uint32_t)(val_offsets[i + 1] - val_offsets[i])) !=
+                SHF_RET_KEY_PUT)
+                break;
+            if (uids_out) uids_out[i] = shf_uid;
+        }
+    free(parts);
     if (!perm_out) free(perm);
     return rc == SHF_HB_OK ? (int64_t)j : rc;
 }

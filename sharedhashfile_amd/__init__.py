@@ -103,6 +103,8 @@ _SIGS = {
     "shf_win_order_async": [_VP, _U64, _VP, _VP, _VP, ctypes.c_size_t, _VP],
     "shf_win_order": [_VP, _U64, _VP, _VP, _INT],
     "shf_hash_batch_fixed_win": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _INT],
+    "shf_uid_parts_batch_fixed_win": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _INT],
+    "shf_uid_parts_batch_var_win": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _INT],
     "shf_hash_batch_var_win": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _INT],
     "shf_hash_batch_fixed_win_async": [_VP, _U32, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP],
     "shf_hash_batch_var_win_async": [_VP, _VP, _U64, _U32, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP],
@@ -628,6 +630,37 @@ def hash_var_win_host(data, offsets, seed=SEED):
                                        perm.ctypes.data, ws.ctypes.data, MEM_HOST)
     _check(rc, "shf_hash_batch_var_win")
     return out, perm, ws
+
+
+def uid_parts_fixed_win_host(keys, key_len=None, seed=SEED):
+    """Host keys in; host (parts uint64[n], perm uint32[n], win_start uint32[257]) out
+    (shf_uid_parts_batch_fixed_win, SHF_HASH_MEM_HOST)."""
+    keys = _np_u8(keys)
+    if key_len is None:
+        key_len = keys.shape[-1] if keys.ndim == 2 else 16
+    flat = keys.reshape(-1)
+    n = flat.size // key_len if key_len else 0
+    parts = np.empty(n, dtype=np.uint64)
+    perm = np.empty(n, dtype=np.uint32)
+    ws = np.empty(257, dtype=np.uint32)
+    _check(load().shf_uid_parts_batch_fixed_win(flat.ctypes.data, key_len, n, seed, parts.ctypes.data,
+                                                perm.ctypes.data, ws.ctypes.data, MEM_HOST),
+           "shf_uid_parts_batch_fixed_win")
+    return parts, perm, ws
+
+
+def uid_parts_var_win_host(data, offsets, seed=SEED):
+    """Variable-length host keys: (parts, perm, win_start) (shf_uid_parts_batch_var_win, SHF_HASH_MEM_HOST)."""
+    data = _np_u8(data).reshape(-1)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = off.size - 1
+    parts = np.empty(n, dtype=np.uint64)
+    perm = np.empty(n, dtype=np.uint32)
+    ws = np.empty(257, dtype=np.uint32)
+    _check(load().shf_uid_parts_batch_var_win(data.ctypes.data, off.ctypes.data, n, seed, parts.ctypes.data,
+                                              perm.ctypes.data, ws.ctypes.data, MEM_HOST),
+           "shf_uid_parts_batch_var_win")
+    return parts, perm, ws
 
 
 def win_order_host(hashes):

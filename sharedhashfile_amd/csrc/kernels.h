@@ -11,8 +11,9 @@ namespace shfhb {
 // kOutHash: 16-B SHF_HASH records; kOutUid: 8-B packed UID parts;
 // kOutProbe: 16-B shf_probe records (row pre-probe), plus the
 // hashes when Sink::hash_out is set; kOutHashWin: the 16-B records plus each
-// key's window byte (h1 & 0xff, shf.c:800) for the window order (win_order.hip).
-enum OutMode { kOutHash = 0, kOutUid = 1, kOutProbe = 2, kOutHashWin = 3 };
+// key's window byte (h1 & 0xff, shf.c:800) for the window order (win_order.hip);
+// kOutUidWin: the 8-B UID parts plus the window byte.
+enum OutMode { kOutHash = 0, kOutUid = 1, kOutProbe = 2, kOutHashWin = 3, kOutUidWin = 4 };
 enum KernelChoice {
   kKernelAuto = 0,
   kKernelFixed16 = 1,
@@ -33,7 +34,7 @@ struct Sink {
   const uint8_t* map8 = nullptr;       // kOutProbe: compact copy of tab_slot (launch_compact_map), or null
   const uint32_t* win_tab = nullptr;
   uint32_t* status = nullptr;  // variable-length keys: set to 1 when a key's offsets are invalid
-  uint8_t* wins = nullptr;     // kOutHashWin: n window bytes (rounded up to whole kWoChunk chunks)
+  uint8_t* wins = nullptr;     // kOutHashWin / kOutUidWin: n window bytes (rounded up to whole kWoChunk chunks)
   uint32_t* win_counts = nullptr;  // kOutHashWin, fused 16-B kernel: each chunk's 256 window counts
   uint16_t* win_sorted = nullptr;  // kOutHashWin, fused 16-B kernel: each chunk's order by window (win_rank.h)
 };

@@ -188,8 +188,9 @@ __device__ __forceinline__ void store_result(const Sink& sink, uint64_t i, const
     const u32x4 v = {(uint32_t)s.h1, (uint32_t)(s.h1 >> 32), (uint32_t)s.h2, (uint32_t)(s.h2 >> 32)};
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(sink.out) + i);
     if constexpr (OUT == kOutHashWin) sink.wins[i] = (uint8_t)s.h1;  // the window, shf.c:800
-  } else if constexpr (OUT == kOutUid) {
+  } else if constexpr (OUT == kOutUid || OUT == kOutUidWin) {
     __builtin_nontemporal_store(uid_parts(s), reinterpret_cast<uint64_t*>(sink.out) + i);
+    if constexpr (OUT == kOutUidWin) sink.wins[i] = (uint8_t)s.h1;  // the window, shf.c:800
   } else {
     store_probe(sink, i, s, probe_row(sink, s));
   }
@@ -1280,6 +1281,8 @@ hipError_t launch_fixed(const void* keys, uint32_t key_len, uint64_t n, uint32_t
       bool ranked = false;
       return launch_fixed_win(keys, key_len, n, seed, sink, st, kernel, &ranked);
     }
+    case kOutUidWin:
+      return launch_fixed_t<kOutUidWin>(keys, key_len, n, seed, sink, st, kernel);
     default:
       return launch_fixed_t<kOutProbe>(keys, key_len, n, seed, sink, st, kernel);
   }
@@ -1312,6 +1315,8 @@ hipError_t launch_var(const void* bytes, const uint64_t* offsets, uint64_t off_b
       return launch_var_t<kOutUid>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     case kOutHashWin:
       return launch_var_t<kOutHashWin>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
+    case kOutUidWin:
+      return launch_var_t<kOutUidWin>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
     default:
       return launch_var_t<kOutProbe>(bytes, offsets, off_base, n, seed, sink, st, kernel, key_bytes);
   }

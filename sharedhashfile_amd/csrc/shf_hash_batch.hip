@@ -508,7 +508,7 @@ struct HostJob {
   bool stage_direct = false;  // else (pageable `hash`): the kernel stores into the slot's pinned staging
   shf_probe* probe = nullptr;
   const shf_row_index* index = nullptr;  // with probe
-  uint8_t* wins = nullptr;  // device: the batch's window bytes (kOutHashWin), key i's at wins[i]
+  uint8_t* wins = nullptr;  // device: the batch's window bytes (kOutHashWin / kOutUidWin), key i's at wins[i]
   size_t rec() const { return uid ? sizeof(uint64_t) : sizeof(shf_hash128); }
   uint8_t* at(void* p, uint64_t i) const { return static_cast<uint8_t*>(p) + i * rec(); }
   int hash_mode() const { return uid ? shfhb::kOutUid : shfhb::kOutHash; }
@@ -668,9 +668,9 @@ void job_sink(const ChunkBufs& b, const HostJob& job, uint64_t i0, shfhb::Sink* 
   } else {
     k->out = job.hash_dev ? job.at(job.hash_dev, i0) : (job.stage_direct && b.hd_out) ? b.hd_out : b.d_out;
     *mode = job.hash_mode();
-    if (job.wins && !job.uid) {
+    if (job.wins) {
       k->wins = job.wins + i0;
-      *mode = shfhb::kOutHashWin;
+      *mode = job.uid ? shfhb::kOutUidWin : shfhb::kOutHashWin;
     }
   }
 }
@@ -678,9 +678,9 @@ void job_sink(const ChunkBufs& b, const HostJob& job, uint64_t i0, shfhb::Sink* 
 // The sink of a whole-batch launch straight into the caller's records (zero copy).
 int direct_sink(const HostJob& job, void* d_out, shfhb::Sink* k) {
   *k = out_sink(d_out);
-  if (!job.wins || job.uid) return job.hash_mode();
+  if (!job.wins) return job.hash_mode();
   k->wins = job.wins;
-  return shfhb::kOutHashWin;
+  return job.uid ? shfhb::kOutUidWin : shfhb::kOutHashWin;
 }
 
 // Results of chunk [i0, i0 + cnt) back to the caller (straight into page-locked
@@ -1332,14 +1332,16 @@ int shf_hash_batch_var_win_async(const void* d_bytes, const uint64_t* d_offsets,
 
 namespace {
 
-// Synchronous hash + window order (shf_hash_batch_{fixed,var}_win). Device
-// memory: the async entry point on the context's stream, then a wait. Host
-// memory: the host pipelines hash into `out` and leave each key's window byte
-// in the device workspace (the records are never copied back in to be
-// ordered), the order is made on the device, and only perm / win_start come
-// back.
-int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n, uint32_t seed,
-                  shf_hash128* out, uint32_t* perm, uint32_t* win_start, int mem) {
+// Synchronous hash + window order (shf_hash_batch_{fixed,var}_win, and with
+// 8-B UID parts instead of the records: shf_uid_parts_batch_{fixed,var}_win).
+// Device memory: the records (or parts) and each key's window byte, then the
+// order from the bytes (16-B records: the fused k_fixed16_win ranks the
+// chunks itself), then a wait. Host memory: the host pipelines write the
+// records (parts) to `out` and leave each key's window byte in the device
+// workspace (the records are never copied back in to be ordered), the order is
+// made on the device, and only perm / win_start come back.
+int hash_win_sync(bool var, bool uid, const void* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                  uint32_t seed, void* out, uint32_t* perm, uint32_t* win_start, int mem) {
   if (mem != SHF_HASH_MEM_DEVICE && mem != SHF_HASH_MEM_HOST) return SHF_HB_ERR_ARG;
   if (n == 0 && !win_start) return SHF_HB_OK;
   if (n > 0xffffffffull || (!var && key_len > kMaxKeyLen)) return SHF_HB_ERR_ARG;
@@ -1353,6 +1355,7 @@ int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t 
   // device memory: on the null stream, as every synchronous device entry point, so the
   // hash and order run after whatever the caller enqueued there (e.g. the keys' producer)
   const hipStream_t st = mem == SHF_HASH_MEM_DEVICE ? nullptr : c->st;
+  const int mode = uid ? shfhb::kOutUidWin : shfhb::kOutHashWin;
   if (mem == SHF_HASH_MEM_DEVICE) {
     shfhb::Sink k = out_sink(out);
     bool ranked = false;
@@ -1361,7 +1364,9 @@ int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t 
       if (var) {
         k.status = c->d_status + 1;
         HB_TRY(hipMemsetAsync(k.status, 0, sizeof(uint32_t), st));
-        HB_TRY(shfhb::launch_var(keys, offsets, 0, n, seed, k, shfhb::kOutHashWin, st));
+        HB_TRY(shfhb::launch_var(keys, offsets, 0, n, seed, k, mode, st));
+      } else if (uid) {
+        HB_TRY(shfhb::launch_fixed(keys, key_len, n, seed, k, mode, st, shfhb::kKernelAuto));
       } else {
         k.win_counts = shfhb::win_order_counts(ws);
         k.win_sorted = shfhb::win_order_sorted(ws, n);
@@ -1376,7 +1381,7 @@ int hash_win_sync(bool var, const void* keys, const uint64_t* offsets, uint32_t 
   uint32_t* d_perm = nullptr;
   if ((rc = ensure_perm(c, n, &d_perm))) return rc;
   if (n) {
-    HostJob job = hash_job(out);
+    HostJob job = uid ? uid_job(static_cast<uint64_t*>(out)) : hash_job(static_cast<shf_hash128*>(out));
     job.wins = shfhb::win_order_wins(ws, n);
     rc = var ? host_var((const uint8_t*)keys, offsets, n, seed, job)
              : host_fixed((const uint8_t*)keys, key_len, n, seed, job);
@@ -1396,13 +1401,25 @@ extern "C" {
 int shf_hash_batch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,
                              uint32_t* perm, uint32_t* win_start, int mem) {
   HB_ENTER();
-  return hash_win_sync(false, keys, nullptr, key_len, n, seed, out, perm, win_start, mem);
+  return hash_win_sync(false, false, keys, nullptr, key_len, n, seed, out, perm, win_start, mem);
 }
 
 int shf_hash_batch_var_win(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed, shf_hash128* out,
                            uint32_t* perm, uint32_t* win_start, int mem) {
   HB_ENTER();
-  return hash_win_sync(true, bytes, offsets, 0, n, seed, out, perm, win_start, mem);
+  return hash_win_sync(true, false, bytes, offsets, 0, n, seed, out, perm, win_start, mem);
+}
+
+int shf_uid_parts_batch_fixed_win(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, uint64_t* parts,
+                                  uint32_t* perm, uint32_t* win_start, int mem) {
+  HB_ENTER();
+  return hash_win_sync(false, true, keys, nullptr, key_len, n, seed, parts, perm, win_start, mem);
+}
+
+int shf_uid_parts_batch_var_win(const void* bytes, const uint64_t* offsets, uint64_t n, uint32_t seed,
+                                uint64_t* parts, uint32_t* perm, uint32_t* win_start, int mem) {
+  HB_ENTER();
+  return hash_win_sync(true, true, bytes, offsets, 0, n, seed, parts, perm, win_start, mem);
 }
 
 int shf_hash_batch_fixed_multi(const void* keys, uint32_t key_len, uint64_t n, uint32_t seed, shf_hash128* out,

@@ -21,7 +21,9 @@
  *      shf_use_uid_parts: a store put from parts is byte-equal to one put from
  *      the full hashes, with the same shf_uid per key, and the reference's
  *      own get finds every key in it; gets and dels with the parts in the seam
- *      give the reference's answers.
+ *      give the reference's answers;
+ *   8. the same put in the window order of the parts (shf_uid_parts_batch_var_win):
+ *      again byte-equal, uids included.
  *
  * TEST INFRASTRUCTURE: built by tests/c/Makefile where /root/reference exists
  * (the reference's headers are needed to compile it), into tests/c/build/, which
@@ -332,6 +334,23 @@ int main(int argc, char **argv)
         return fail("shf_uid_parts_batch_fixed");
     for (uint64_t i = 0; i < nf; ++i)
         if (fparts[i] != parts_of(&fh[i])) return fail("fixed UID parts != the parts of the GPU hash");
+    /* 8. the window-ordered put from UID parts (shf_put_batch_var_parts_win_ordered): a stable order
+     *    by the parts' window, and the store byte-equal, uids included, to the full-hash put */
+    SHF *oshf = shf_attach(folder, "seamuidwin", 0);
+    if (!oshf) return fail("shf_attach uid parts window order");
+    uint32_t *operm = malloc(n_put * sizeof *operm), *ouid = malloc(n_put * sizeof *ouid);
+    if (shf_put_batch_var_parts_win_ordered(oshf, bytes, off, n_put, vals, voff, operm, ouid) != (int64_t)n_put)
+        return fail("shf_put_batch_var_parts_win_ordered");
+    for (uint64_t j = 1; j < n_put; ++j)
+        if ((parts[operm[j]] & 0xff) < (parts[operm[j - 1]] & 0xff) ||
+            ((parts[operm[j]] & 0xff) == (parts[operm[j - 1]] & 0xff) && operm[j] < operm[j - 1]))
+            return fail("uid parts window order: not a stable sort by window");
+    uint64_t ouid_same = 0;
+    for (uint64_t i = 0; i < n_put; ++i) ouid_same += ouid[i] == uid_h[i];
+    if (ouid_same != n_put) return fail("uid parts window order: shf_uid differs from the full-hash put");
+    const int64_t owin_same_files = same_store_files(folder, "seamuidh", hshf, "seamuidwin", oshf);
+    if (owin_same_files < 0) return fail("uid parts window order: tab files differ from the full-hash put");
+    shf_detach(oshf);
     shf_detach(hshf);
     shf_detach(pshf);
 
@@ -339,13 +358,14 @@ int main(int argc, char **argv)
            "\"probed_fast\": %llu, \"slots\": %lld, \"fixed_found\": %llu, \"win_order_same_tab_files\": %lld, "
            "\"win_order_found\": %llu, \"win_range_put\": %lld, \"parts_same_uids\": %llu, "
            "\"parts_same_tab_files\": %lld, \"parts_ref_found\": %llu, \"parts_get_found\": %llu, "
-           "\"parts_deleted\": %llu, \"parts_left\": %llu}\n",
+           "\"parts_deleted\": %llu, \"parts_left\": %llu, \"parts_win_same_uids\": %llu, "
+           "\"parts_win_same_tab_files\": %lld}\n",
            (unsigned long long)n_put, (unsigned long long)n, (unsigned long long)ref_found,
            (unsigned long long)ref_right, (unsigned long long)found, (unsigned long long)fast, (long long)slots,
            (unsigned long long)ffound, (long long)same_files, (unsigned long long)wfound2,
            (long long)range_put, (unsigned long long)uid_same, (long long)parts_same_files,
            (unsigned long long)pright, (unsigned long long)pgot, (unsigned long long)pdel,
-           (unsigned long long)pleft);
+           (unsigned long long)pleft, (unsigned long long)ouid_same, (long long)owin_same_files);
     shf_detach(wshf);
     /* the stores' files go with the folder (shf_del would run `du` and `rm` through popen) */
     shf_detach(shf);

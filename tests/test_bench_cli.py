@@ -216,7 +216,8 @@ def test_stdout_line_fits_the_driver_tail_at_one_and_eight_ranks():
           "ceilings_gbs": {"h2d": 55.71, "d2h": 56.12, "both_h2d": 40.17, "both_d2h": 40.33, "both": 80.44,
                            "h2d_pageable": 51.32, "bytes_per_copy": 160000000}}
     for k in ("fixed16_pageable", "fixed16_pinned", "fixed16_pinned_staged", "var_pageable", "var_pinned",
-              "fixed16_pageable_x16", "uid16_pageable", "uid16_pinned", "uid16_pinned_staged"):
+              "fixed16_pageable_x16", "uid16_pageable", "uid16_pinned", "uid16_pinned_staged", "hashwin16_pageable",
+              "uidwin16_pageable"):
         hi[k] = {"value": 2.5e9, "value_min": 2.4123e9, "value_max": 2.6123e9, "repeats": 5, "wire_bytes": 32.0,
                  "pcie_bound": 2.51375e9, "frac_of_pcie": 0.995}
     for world in (1, 8):
@@ -236,8 +237,8 @@ def test_stdout_line_fits_the_driver_tail_at_one_and_eight_ranks():
         assert len(bench.json.dumps(full)) > len(s)  # the detail record keeps what the line drops
     _, line1 = _compact(1, cpu, hi)
     assert line1["cpu_baseline"]["kind"] == "reference" and line1["cpu_baseline"]["multi"]["cores"] == 16
-    assert line1["host_inclusive"]["fixed16_pinned"] == [2.5e9, 0.995]  # [keys/s, frac_of_pcie]
-    assert line1["host_inclusive"]["uid16_pageable"] == [2.5e9, 0.995]
+    assert line1["host_inclusive"]["fixed16_pinned"] == [2.5, 0.995]  # [G keys/s, frac_of_pcie]
+    assert line1["host_inclusive"]["uid16_pageable"] == [2.5, 0.995] and line1["host_inclusive"]["unit"] == "G keys/s"
     assert line1["host_inclusive"]["pcie_gbs"] == {"h2d": 55.71, "d2h": 56.12, "both": 80.44, "h2d_pageable": 51.32}
     _, line8 = _compact(8)
     assert "per_rank" not in line8 and line8["slowest_over_fastest_rank"]["fixed16"] == round(57.0 / 50.0, 4)

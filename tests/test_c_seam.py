@@ -71,6 +71,8 @@ def test_seam_program_put_and_probed_get():
     assert r["parts_same_uids"] == r["n_put"] and r["parts_same_tab_files"] >= 256
     assert r["parts_ref_found"] == r["parts_get_found"] == r["n_put"]
     assert r["parts_deleted"] == r["parts_left"] == r["n_put"] // 2  # del through the parts, then the CPU get
+    # the window-ordered put from parts + order (12 B per key back instead of 20): the same store and uids
+    assert r["parts_win_same_uids"] == r["n_put"] and r["parts_win_same_tab_files"] >= 256
 
 
 @pytest.mark.gpu

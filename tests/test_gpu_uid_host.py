@@ -224,3 +224,70 @@ def test_host_uid_mixed_and_unaligned_buffers(hb, dev, oracle, monkeypatch):
     big = (1 << 20) + 4099  # longer than a 1-MiB slot: one key at a time through a device buffer of its own
     kb = np.frombuffer(splitmix_bytes(3 * big, 341), dtype=np.uint8)
     assert np.array_equal(hb.uid_parts_fixed_host(kb, big), _want_fixed(oracle, kb, big))
+
+
+def _want_order(parts):
+    w = (parts & np.uint64(0xFF)).astype(np.int64)
+    perm = np.argsort(w, kind="stable").astype(np.uint32)
+    ws = np.zeros(257, dtype=np.uint32)
+    ws[1:] = np.cumsum(np.bincount(w, minlength=256))
+    return perm, ws
+
+
+@pytest.mark.parametrize("key_len", [16, 24, 256])
+def test_uid_parts_win_host_fixed(hb, dev, oracle, key_len):
+    """shf_uid_parts_batch_fixed_win, host memory: the parts, and the window
+    order a stable sort of their window byte gives (= shf_win_order of the
+    batch's hashes), with each window's first position."""
+    n = 1_000_003
+    flat = np.frombuffer(splitmix_bytes(n * key_len, 350 + key_len), dtype=np.uint8)
+    parts, perm, ws = hb.uid_parts_fixed_win_host(flat, key_len)
+    want = _want_fixed(oracle, flat, key_len)
+    assert np.array_equal(parts, want)
+    wp, wws = _want_order(want)
+    assert np.array_equal(perm, wp) and np.array_equal(ws, wws)
+
+
+def test_uid_parts_win_var_and_device(hb, dev, oracle):
+    """The variable-length form from host memory, both forms on device memory,
+    n = 0 (win_start all zero) and a decreasing offset (refused before any copy)."""
+    rng = np.random.default_rng(360)
+    m = 300_001
+    lens = rng.integers(0, 600, size=m)
+    off = np.zeros(m + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    want = oracle.uid_parts(oracle.hash_var(data, off))
+    wp, wws = _want_order(want)
+    parts, perm, ws = hb.uid_parts_var_win_host(data, off)
+    assert np.array_equal(parts, want) and np.array_equal(perm, wp) and np.array_equal(ws, wws)
+    lib = hb.load()
+    d_data = torch.from_numpy(data).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_parts = torch.empty(m, dtype=torch.int64, device=dev)
+    d_perm = torch.empty(m, dtype=torch.int32, device=dev)
+    d_ws = torch.empty(257, dtype=torch.int32, device=dev)
+    assert lib.shf_uid_parts_batch_var_win(d_data.data_ptr(), d_off.data_ptr(), m, 12345, d_parts.data_ptr(),
+                                           d_perm.data_ptr(), d_ws.data_ptr(), hb.MEM_DEVICE) == 0
+    assert np.array_equal(d_parts.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(d_perm.cpu().numpy().view(np.uint32), wp)
+    assert np.array_equal(d_ws.cpu().numpy().view(np.uint32), wws)
+    n = 500_000
+    keys = torch.randint(0, 256, (n * 16,), dtype=torch.uint8, device=dev)
+    f_parts = torch.empty(n, dtype=torch.int64, device=dev)
+    f_perm = torch.empty(n, dtype=torch.int32, device=dev)
+    assert lib.shf_uid_parts_batch_fixed_win(keys.data_ptr(), 16, n, 12345, f_parts.data_ptr(), f_perm.data_ptr(),
+                                             None, hb.MEM_DEVICE) == 0
+    fwant = _want_fixed(oracle, keys.cpu().numpy(), 16)
+    assert np.array_equal(f_parts.cpu().numpy().view(np.uint64), fwant)
+    assert np.array_equal(f_perm.cpu().numpy().view(np.uint32), _want_order(fwant)[0])
+    z = np.full(257, 7, dtype=np.uint32)
+    assert lib.shf_uid_parts_batch_fixed_win(None, 16, 0, 12345, None, None, z.ctypes.data, hb.MEM_HOST) == 0
+    assert not z.any()
+    bad = off.copy()
+    bad[10] = bad[9] - np.uint64(1)
+    out = np.zeros(m, dtype=np.uint64)
+    pm = np.zeros(m, dtype=np.uint32)
+    assert lib.shf_uid_parts_batch_var_win(data.ctypes.data, bad.ctypes.data, m, 12345, out.ctypes.data,
+                                           pm.ctypes.data, None, hb.MEM_HOST) == hb.ERR_ARG
+    assert not out.any()
