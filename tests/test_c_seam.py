@@ -40,6 +40,53 @@ def test_seam_header_compiles_against_reference_headers():
     assert p.returncode == 0, p.stderr.decode()
 
 
+def test_use_uid_parts_gives_shf_c_the_same_bits(tmp_path):
+    """shf_use_uid_parts() against shf_use_hash(), on the CPU: for 2M random
+    hashes (and the all-ones / all-zero edge cases), the win / tab2 / row / rnd
+    that put and find compute from shf_hash (/root/reference/src/shf.c:800-803,
+    :893-896, restated with the reference's own SHF_* constants) are the same
+    from the parts word as from the full hash, and every other byte is zero."""
+    if not os.path.isdir("/root/reference/src"):
+        pytest.skip("reference headers absent")
+    src = r"""
+#include "shf.private.h"
+#include "shf.h"
+#include "shf_hash_batch_shf.h"
+#include <stdio.h>
+__thread SHF_HASH shf_hash; __thread const char *shf_hash_key; __thread uint32_t shf_hash_key_len;
+static uint64_t sm(uint64_t *s) { uint64_t z = (*s += 0x9e3779b97f4a7c15ull); z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+                                  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull; return z ^ (z >> 31); }
+static void bits(uint32_t *b) {
+    b[0] = shf_hash.u16[0] % SHF_WINS_PER_SHF; b[1] = shf_hash.u16[1] % SHF_TABS_PER_WIN;
+    b[2] = shf_hash.u16[2] % SHF_ROWS_PER_TAB; b[3] = shf_hash.u32[2] % (1 << (32 - SHF_TABS_PER_WIN_BITS)); }
+int main(void) {
+    uint64_t st = 42, bad = 0;
+    for (uint64_t i = 0; i < 2000000; ++i) {
+        shf_hash128 h = {sm(&st), sm(&st)};
+        if (i == 0) h.h1 = h.h2 = ~0ull;
+        if (i == 1) h.h1 = h.h2 = 0;
+        uint32_t a[4], b[4];
+        shf_use_hash("k", 1, &h); bits(a);
+        const uint64_t parts = (h.h1 & 0xff) | ((h.h1 >> 16) & 0x7ff) << 8 | ((h.h1 >> 32) & 0x1ff) << 19 |
+                               (h.h2 & 0x1fffff) << 32;  /* what the kernels pack (kernels: uid_parts) */
+        shf_use_uid_parts("k", 1, parts); bits(b);
+        bad += memcmp(a, b, sizeof a) != 0 || shf_hash.u16[3] || shf_hash.u32[3] || shf_hash_key_len != 1;
+    }
+    printf("%llu\n", (unsigned long long)bad);
+    return bad != 0;
+}
+"""
+    c = tmp_path / "uidbits.c"
+    c.write_text(src)
+    exe = tmp_path / "uidbits"
+    p = subprocess.run(["gcc", "-O1", "-std=gnu99", "-Wall", "-Wno-address-of-packed-member", "-I",
+                        os.path.join(ROOT, "include"), "-I", "/root/reference/src", str(c), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout + r.stderr
+
+
 def test_seam_header_refuses_without_reference_private_header():
     src = '#include "shf_hash_batch_shf.h"\nint main(void){return 0;}\n'
     p = subprocess.run(["gcc", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), "-x", "c", "-"],
